@@ -1,0 +1,143 @@
+/*
+ * ibldpc.h — C ABI of the MI355X-native batched LDPC decoding engine (libibldpc.so).
+ *
+ * Drop-in boundary for the reference's decoder classes (mx-strk/InformationBottleneckDecodingLDPC,
+ * snapshot 2024-10-22).  Each entry point names the reference interface it replaces; the
+ * Python classes in informationbottleneckdecodingldpc_amd/ keep the reference's method
+ * names and call these through ctypes.
+ *
+ * Conventions
+ *   - return 0 (IBL_OK) or a negative IBL_E* code; the message of the last failure on the
+ *     calling thread is returned by ibl_last_error();
+ *   - d_* pointers are DEVICE pointers owned by the caller (e.g. torch ROCm tensors'
+ *     data_ptr() or hipMalloc); `stream` is a hipStream_t (NULL = default stream);
+ *   - decode calls are asynchronous on `stream` and never synchronise the host
+ *     (the reference reads the syndrome back every iteration; here the early stop is
+ *     decided on the device);
+ *   - a handle owns its device tables and scratch, is bound to the device it was created
+ *     on and is not thread-safe (as the reference's decoder objects, which own their inboxes);
+ *   - arrays are [row][codeword] with row stride B (the reference's received_blocks layout).
+ */
+#ifndef IBLDPC_H
+#define IBLDPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IBL_VERSION 1
+
+enum { IBL_OK = 0, IBL_EINVAL = -1, IBL_EHIP = -2, IBL_ENOMEM = -3, IBL_EUNSUPPORTED = -4 };
+enum { IBL_U8 = 1, IBL_I32 = 2, IBL_F32 = 3, IBL_F64 = 4 };
+enum { IBL_MINSUM = 0, IBL_BP = 1 };
+enum { IBL_FLAG_FORCE_GENERIC = 1 };
+
+typedef struct ibl_graph ibl_graph;
+typedef struct ibl_ib ibl_ib;
+typedef struct ibl_float ibl_float;
+
+int ibl_version(void);
+const char* ibl_last_error(void);
+/* number of visible HIP devices (0 on a machine without GPU) */
+int ibl_device_count(int32_t* n);
+
+/*
+ * Tanner-graph index construction on the HOST (no device needed).
+ * Replaces map_node_connections (Discrete_LDPC_decoding/discrete_LDPC_decoder_irreg.py:121-170;
+ * regular copy discrete_LDPC_decoder.py:88-130).  Input: canonical CSR of H (column indices
+ * strictly ascending within each row).  Outputs (caller-allocated): cn_start[n_c], cn_deg[n_c],
+ * tgt_cn[E] (= target_memory_cells_checknodes), vn_start[n_v], vn_deg[n_v],
+ * tgt_vn[E] (= target_memory_cells_varnodes).
+ */
+int ibl_map_node_connections(int32_t n_v, int32_t n_c, const int32_t* csr_indptr, const int32_t* csr_cols,
+                             int32_t* cn_start, int32_t* cn_deg, int32_t* tgt_cn,
+                             int32_t* vn_start, int32_t* vn_deg, int32_t* tgt_vn);
+
+/*
+ * Upload a code graph to `device` (host arrays in, canonical CSR of H).
+ * Replaces the index-array upload half of init_OpenCL_decoding
+ * (discrete_LDPC_decoder_irreg.py:191-204, min_sum_decoder_irreg.py:182-195).
+ */
+int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* csr_indptr, const int32_t* csr_cols,
+                     int32_t device, ibl_graph** out);
+int ibl_graph_info(const ibl_graph* g, int32_t* n_v, int32_t* n_c, int64_t* n_e, int32_t* d_c_max,
+                   int32_t* d_v_max);
+void ibl_graph_destroy(ibl_graph* g);
+
+/*
+ * Information-bottleneck (integer lookup-table) decoder.
+ * Replaces Discrete_LDPC_Decoder_class_irregular.init_OpenCL_decoding
+ * (discrete_LDPC_decoder_irreg.py:172-243) and Discrete_LDPC_Decoder_class.init_OpenCL_decoding
+ * (discrete_LDPC_decoder.py:132-200): uploads the CN / VN LUT vectors (reference layout, int32,
+ * entries in [0, T_dec)), the matching vectors (irregular class; ignored unless match != 0) and
+ * allocates inboxes for up to max_batch codewords (`msg_at_time`).  The CN/VN vector lengths
+ * must be at least the reference's (T_ch^2 + (CM-3) T_ch T + (I-1)(CM-2) T^2, resp.
+ * I (T_ch T + (VM-1) T^2), CM/VM = the graph's maximum check/variable degree).
+ * Fast path (LDS-resident tables) when T_ch == T_dec <= 16 and all degrees <= 16; otherwise a
+ * generic reference-indexing path.  flags: IBL_FLAG_FORCE_GENERIC.
+ */
+int ibl_ib_create(const ibl_graph* g, int32_t T_ch, int32_t T_dec, int32_t imax,
+                  const int32_t* cn_lut, int64_t cn_len, const int32_t* vn_lut, int64_t vn_len,
+                  const int32_t* match_cn, int64_t mc_len, const int32_t* match_vn, int64_t mv_len,
+                  int32_t match, int32_t max_batch, int32_t flags, ibl_ib** out);
+/* 1 = LDS fast path, 0 = generic path */
+int ibl_ib_path(const ibl_ib* h);
+/*
+ * Decode B codewords.  Replaces decode_OpenCL (discrete_LDPC_decoder_irreg.py:245-341;
+ * discrete_LDPC_decoder.py:202-295).
+ *   d_ch   [N][B] channel cluster ids (IBL_U8 or IBL_I32), values in [0, T_ch)
+ *   d_out  [N][B] decided cluster ids (IBL_U8 or IBL_I32); bit = (id < T_dec/2)
+ *   early_stop  1: stop when the whole batch has zero syndrome (reference behaviour);
+ *               0: run exactly imax iterations (benchmark / decode_on_host behaviour)
+ *   d_iters     optional device int32 receiving the iteration index used for the output
+ *               (the reference's i_num - 1), NULL to skip
+ */
+int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void* d_out, int32_t out_dtype,
+                  int32_t early_stop, int32_t* d_iters, void* stream);
+void ibl_ib_destroy(ibl_ib* h);
+/*
+ * Kernel timing for the benchmark (no reference counterpart): when enabled, every check-node and
+ * variable-node launch of ibl_ib_decode / ibl_float_decode is bracketed by HIP events on the
+ * decode stream.  *_read synchronises those events, returns the summed milliseconds and launch
+ * counts since the last read (kernels that exited early through the stop flags included), and
+ * clears them.
+ */
+int ibl_ib_timing(ibl_ib* h, int32_t enable);
+int ibl_ib_timing_read(ibl_ib* h, double* cn_ms, int32_t* cn_launches, double* vn_ms, int32_t* vn_launches);
+
+/*
+ * Float min-sum / belief-propagation decoder.
+ * Replaces Min_Sum_Decoder_class_irregular / BeliefPropagationDecoderClassIrregular
+ * .init_OpenCL_decoding (min_sum_decoder_irreg.py:167-218, bp_decoder_irreg.py:167-218).
+ * kind = IBL_MINSUM | IBL_BP; precision = IBL_F32 (BASELINE build) | IBL_F64 (the reference's
+ * double precision); llr_max = clamp of BP / VN messages (the reference's LLR_MAX = 150).
+ */
+int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_max, int32_t precision,
+                     int32_t max_batch, ibl_float** out);
+/*
+ * Replaces decode_OpenCL_min_sum (min_sum_decoder_irreg.py:221-287) and
+ * decode_OpenCL_belief_propagation (bp_decoder_irreg.py:221-286).
+ *   d_llr [N][B] channel LLRs (IBL_F32 / IBL_F64), d_out [N][B] APP LLRs (IBL_F32 / IBL_F64)
+ */
+int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out,
+                     int32_t out_dtype, int32_t early_stop, int32_t* d_iters, void* stream);
+void ibl_float_destroy(ibl_float* h);
+int ibl_float_timing(ibl_float* h, int32_t enable);
+int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_launches, double* vn_ms, int32_t* vn_launches);
+
+/*
+ * Error counter.  Replaces return_errors_all_zero (discrete_LDPC_decoder_irreg.py:343-349,
+ * discrete_LDPC_decoder.py:297-300, min_sum_decoder_irreg.py:290-295): counts entries
+ * x[r][b] < threshold for r < rows, b < B (row stride ld) into the device int64 *d_count
+ * (overwritten).  IB: threshold = T_dec/2; float: threshold = 0.
+ */
+int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
+                    int64_t* d_count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IBLDPC_H */

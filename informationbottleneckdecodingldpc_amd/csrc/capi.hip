@@ -1,0 +1,632 @@
+// C ABI (include/ibldpc.h): handle management, table preparation and the decode schedules.
+//
+// Schedules restate the reference's host loops without their per-iteration host sync:
+//   IB:    decode_OpenCL            (Discrete_LDPC_decoding/discrete_LDPC_decoder_irreg.py:245-341)
+//   float: decode_OpenCL_min_sum    (Continous_LDPC_Decoding/min_sum_decoder_irreg.py:221-287)
+//          decode_OpenCL_belief_propagation (bp_decoder_irreg.py:221-286)
+// Early stop: each check-node pass ORs "some check unsatisfied" into 64 flag words of its
+// iteration; the launches of the next iteration read those words and exit at once when they
+// are all zero, and a one-wave kernel turns the flags into the iteration index the output
+// pass uses.  The host only enqueues.
+#include <algorithm>
+#include <functional>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "ibldpc.h"
+
+using namespace ibl;
+
+static thread_local std::string g_err;
+static inline void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess)                                                                   \
+      return fail(IBL_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));            \
+  } while (0)
+
+template <typename T>
+static int dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) return fail(IBL_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return IBL_OK;
+}
+template <typename T>
+static int dupload(T** p, const T* h, size_t count) {
+  int rc = dalloc(p, count);
+  if (rc) return rc;
+  if (count) HIPCHK(hipMemcpy(*p, h, count * sizeof(T), hipMemcpyHostToDevice));
+  return IBL_OK;
+}
+
+struct ibl_graph {
+  int device = 0, num_cus = 256;
+  int32_t n_v = 0, n_c = 0;
+  int64_t n_e = 0;
+  int32_t dcm = 0, dvm = 0;
+  std::vector<int32_t> h_cn_deg, h_vn_deg;
+  int32_t *cn_start = nullptr, *cn_deg = nullptr, *tgt_cn = nullptr;
+  int32_t *vn_start = nullptr, *vn_deg = nullptr, *tgt_vn = nullptr, *csr_cols = nullptr;
+};
+
+// HIP-event timing of the CN / VN launches (benchmark only).
+struct KTimer {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  std::vector<std::pair<int, int>> pending;  // (kind 0=CN 1=VN, first event index)
+  size_t next = 0;
+  int mark(hipStream_t s) {
+    if (next == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return -1;
+      pool.push_back(e);
+    }
+    (void)hipEventRecord(pool[next], s);
+    return (int)next++;
+  }
+  template <typename F>
+  hipError_t timed(int kind, hipStream_t s, F&& launch) {
+    if (!on) return launch();
+    const int a = mark(s);
+    hipError_t e = launch();
+    mark(s);
+    if (a >= 0) pending.emplace_back(kind, a);
+    return e;
+  }
+  int read(double* cn_ms, int32_t* cn_n, double* vn_ms, int32_t* vn_n) {
+    double ms[2] = {0, 0};
+    int32_t n[2] = {0, 0};
+    for (auto& p : pending) {
+      if (hipEventSynchronize(pool[p.second + 1]) != hipSuccess) return -1;
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, pool[p.second], pool[p.second + 1]) != hipSuccess) return -1;
+      ms[p.first] += t;
+      n[p.first] += 1;
+    }
+    pending.clear();
+    next = 0;
+    if (cn_ms) *cn_ms = ms[0];
+    if (cn_n) *cn_n = n[0];
+    if (vn_ms) *vn_ms = ms[1];
+    if (vn_n) *vn_n = n[1];
+    return 0;
+  }
+  ~KTimer() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+struct KCfg {
+  int grid = 0, block = 256;
+  size_t lds = 0;
+};
+
+struct ibl_ib {
+  const ibl_graph* g = nullptr;
+  int32_t Tc = 0, T = 0, imax = 0, CM = 0, VM = 0, match = 0, max_batch = 0, ldb = 0;
+  bool fast = false;
+  uint8_t *cin = nullptr, *vin = nullptr, *ch8 = nullptr;
+  int32_t *flags = nullptr, *dL = nullptr;
+  // fast path
+  uint32_t *cn_img = nullptr, *vn_img = nullptr, *dec_img = nullptr;
+  int cn_nt = 0, vn_nt = 0, dec_nt = 0;
+  int32_t cn_fslot[kMaxD + 1] = {0}, vn_fslot[kMaxD + 1] = {0};
+  KCfg kcn, kvn, kdec;
+  KTimer timer;
+  // generic path
+  int32_t *cn_lut = nullptr, *vn_lut = nullptr, *mc = nullptr, *mv = nullptr;
+  int64_t cn_len = 0, vn_len = 0, mc_len = 0, mv_len = 0;
+};
+
+struct ibl_float {
+  const ibl_graph* g = nullptr;
+  int32_t kind = 0, imax = 0, prec = kF32, max_batch = 0, ldb = 0;
+  double llr_max = 150.0;
+  void *cin = nullptr, *vbuf0 = nullptr, *vbuf1 = nullptr, *chf = nullptr;
+  int32_t *flags = nullptr, *dL = nullptr;
+  int grid_cn = 0, grid_vn = 0;
+  KTimer timer;
+};
+
+extern "C" {
+
+int ibl_version(void) { return IBL_VERSION; }
+const char* ibl_last_error(void) { return g_err.c_str(); }
+
+int ibl_device_count(int32_t* n) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (n) *n = (e == hipSuccess) ? c : 0;
+  return IBL_OK;
+}
+
+int ibl_map_node_connections(int32_t n_v, int32_t n_c, const int32_t* indptr, const int32_t* cols,
+                             int32_t* cn_start, int32_t* cn_deg, int32_t* tgt_cn, int32_t* vn_start,
+                             int32_t* vn_deg, int32_t* tgt_vn) {
+  if (n_v <= 0 || n_c <= 0 || !indptr || !cols) return fail(IBL_EINVAL, "empty graph");
+  if (indptr[0] != 0) return fail(IBL_EINVAL, "csr_indptr[0] must be 0");
+  const int64_t E = indptr[n_c];
+  std::vector<int32_t> vdeg(n_v, 0);
+  for (int32_t c = 0; c < n_c; ++c) {
+    if (indptr[c + 1] < indptr[c]) return fail(IBL_EINVAL, "csr_indptr not monotone");
+    for (int32_t e = indptr[c]; e < indptr[c + 1]; ++e) {
+      if (cols[e] < 0 || cols[e] >= n_v) return fail(IBL_EINVAL, "column index out of range");
+      if (e > indptr[c] && cols[e] <= cols[e - 1])
+        return fail(IBL_EINVAL, "column indices must be strictly ascending within a row (canonical CSR)");
+      vdeg[cols[e]]++;
+    }
+    cn_start[c] = indptr[c];
+    cn_deg[c] = indptr[c + 1] - indptr[c];
+  }
+  int64_t acc = 0;
+  for (int32_t v = 0; v < n_v; ++v) {
+    vn_start[v] = (int32_t)acc;
+    vn_deg[v] = vdeg[v];
+    acc += vdeg[v];
+  }
+  // walking checks in ascending order fills each variable's edges in ascending row order
+  std::vector<int64_t> fill(vn_start, vn_start + n_v);
+  for (int32_t c = 0; c < n_c; ++c)
+    for (int32_t e = indptr[c]; e < indptr[c + 1]; ++e) {
+      const int64_t p = fill[cols[e]]++;
+      tgt_cn[e] = (int32_t)p;
+      tgt_vn[p] = e;
+    }
+  (void)E;
+  return IBL_OK;
+}
+
+int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int32_t* cols, int32_t device,
+                     ibl_graph** out) {
+  if (!out) return fail(IBL_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n_v <= 0 || n_c <= 0) return fail(IBL_EINVAL, "empty graph");
+  const int64_t E = indptr[n_c];
+  std::vector<int32_t> cs(n_c), cd(n_c), tc(E), vs(n_v), vd(n_v), tv(E);
+  int rc = ibl_map_node_connections(n_v, n_c, indptr, cols, cs.data(), cd.data(), tc.data(), vs.data(), vd.data(),
+                                    tv.data());
+  if (rc) return rc;
+  for (int32_t c = 0; c < n_c; ++c)
+    if (cd[c] < 2 || cd[c] > 255) return fail(IBL_EUNSUPPORTED, "check-node degrees must lie in [2, 255]");
+  for (int32_t v = 0; v < n_v; ++v)
+    if (vd[v] < 1 || vd[v] > 255) return fail(IBL_EUNSUPPORTED, "variable-node degrees must lie in [1, 255]");
+  HIPCHK(hipSetDevice(device));
+  auto* g = new ibl_graph();
+  g->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) g->num_cus = prop.multiProcessorCount;
+  g->n_v = n_v;
+  g->n_c = n_c;
+  g->n_e = E;
+  g->dcm = *std::max_element(cd.begin(), cd.end());
+  g->dvm = *std::max_element(vd.begin(), vd.end());
+  g->h_cn_deg = cd;
+  g->h_vn_deg = vd;
+  if ((rc = dupload(&g->cn_start, cs.data(), n_c)) || (rc = dupload(&g->cn_deg, cd.data(), n_c)) ||
+      (rc = dupload(&g->tgt_cn, tc.data(), E)) || (rc = dupload(&g->vn_start, vs.data(), n_v)) ||
+      (rc = dupload(&g->vn_deg, vd.data(), n_v)) || (rc = dupload(&g->tgt_vn, tv.data(), E)) ||
+      (rc = dupload(&g->csr_cols, cols, E))) {
+    ibl_graph_destroy(g);
+    return rc;
+  }
+  *out = g;
+  return IBL_OK;
+}
+
+int ibl_graph_info(const ibl_graph* g, int32_t* n_v, int32_t* n_c, int64_t* n_e, int32_t* dcm, int32_t* dvm) {
+  if (!g) return fail(IBL_EINVAL, "graph is NULL");
+  if (n_v) *n_v = g->n_v;
+  if (n_c) *n_c = g->n_c;
+  if (n_e) *n_e = g->n_e;
+  if (dcm) *dcm = g->dcm;
+  if (dvm) *dvm = g->dvm;
+  return IBL_OK;
+}
+
+void ibl_graph_destroy(ibl_graph* g) {
+  if (!g) return;
+  (void)hipSetDevice(g->device);
+  dfree(g->cn_start); dfree(g->cn_deg); dfree(g->tgt_cn);
+  dfree(g->vn_start); dfree(g->vn_deg); dfree(g->tgt_vn); dfree(g->csr_cols);
+  delete g;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ IB table images
+namespace {
+
+using Table = std::vector<uint8_t>;  // 256 entries, (t, m) at t*16 + m
+
+Table make_table(int T, const std::function<int(int, int)>& f) {
+  Table tb(256, 0);
+  for (int t = 0; t < T; ++t)
+    for (int m = 0; m < T; ++m) tb[t * kTP + m] = (uint8_t)f(t, m);
+  return tb;
+}
+
+void append(std::vector<uint32_t>& img, const Table& tb) {
+  for (int r = 0; r < 64; ++r)
+    img.push_back((uint32_t)tb[4 * r] | ((uint32_t)tb[4 * r + 1] << 8) | ((uint32_t)tb[4 * r + 2] << 16) |
+                  ((uint32_t)tb[4 * r + 3] << 24));
+}
+
+std::vector<int> present(const std::vector<int32_t>& deg) {
+  std::vector<int> d(deg.begin(), deg.end());
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  return d;
+}
+
+int pick_cfg(int which, int maxd, int nt, int num_cus, KCfg* k) {
+  k->lds = (size_t)nt * kTbl;
+  int best_waves = 0;
+  for (int block : {512, 1024, 256}) {
+    int bpc = 0;
+    if (ib_fast_occupancy(which, maxd, block, k->lds, &bpc) != hipSuccess) continue;
+    const int waves = bpc * block / 64;
+    if (bpc > 0 && waves > best_waves) {
+      best_waves = waves;
+      k->block = block;
+      k->grid = bpc * num_cus;
+    }
+  }
+  return best_waves > 0 ? IBL_OK : fail(IBL_EHIP, "no occupancy for IB kernel (LDS too large?)");
+}
+
+}  // namespace
+
+extern "C" {
+
+int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const int32_t* cn_lut, int64_t cn_len,
+                  const int32_t* vn_lut, int64_t vn_len, const int32_t* match_cn, int64_t mc_len,
+                  const int32_t* match_vn, int64_t mv_len, int32_t match, int32_t max_batch, int32_t flags,
+                  ibl_ib** out) {
+  if (!out) return fail(IBL_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!g) return fail(IBL_EINVAL, "graph is NULL");
+  if (Tc < 2 || T < 2 || Tc > 256 || T > 256) return fail(IBL_EUNSUPPORTED, "cardinalities must lie in [2, 256]");
+  if (imax < 1) return fail(IBL_EINVAL, "imax must be >= 1");
+  if (max_batch < 1) return fail(IBL_EINVAL, "max_batch must be >= 1");
+  const int CM = g->dcm, VM = g->dvm;
+  if (CM < 3) return fail(IBL_EUNSUPPORTED, "IB decoding needs a check-node degree >= 3");
+  const int64_t need_cn = (int64_t)Tc * Tc + (int64_t)(CM - 3) * Tc * T + (int64_t)(imax - 1) * (CM - 2) * T * T;
+  const int64_t need_vn = (int64_t)imax * ((int64_t)Tc * T + (int64_t)(VM - 1) * T * T);
+  if (!cn_lut || cn_len < need_cn) return fail(IBL_EINVAL, "CN LUT vector shorter than the reference layout");
+  if (!vn_lut || vn_len < need_vn) return fail(IBL_EINVAL, "VN LUT vector shorter than the reference layout");
+  for (int64_t i = 0; i < cn_len; ++i)
+    if (cn_lut[i] < 0 || cn_lut[i] >= T) return fail(IBL_EINVAL, "CN LUT entries must lie in [0, T_dec)");
+  for (int64_t i = 0; i < vn_len; ++i)
+    if (vn_lut[i] < 0 || vn_lut[i] >= T) return fail(IBL_EINVAL, "VN LUT entries must lie in [0, T_dec)");
+  if (match) {
+    if (!match_cn || mc_len < (int64_t)imax * CM * T || !match_vn || mv_len < (int64_t)imax * VM * T)
+      return fail(IBL_EINVAL, "matching vectors shorter than (imax, d_max, T_dec)");
+    for (int64_t i = 0; i < mc_len; ++i)
+      if (match_cn[i] < 0 || match_cn[i] >= T) return fail(IBL_EINVAL, "matching entries must lie in [0, T_dec)");
+    for (int64_t i = 0; i < mv_len; ++i)
+      if (match_vn[i] < 0 || match_vn[i] >= T) return fail(IBL_EINVAL, "matching entries must lie in [0, T_dec)");
+  }
+  HIPCHK(hipSetDevice(g->device));
+  auto* h = new ibl_ib();
+  h->g = g;
+  h->Tc = Tc; h->T = T; h->imax = imax; h->CM = CM; h->VM = VM; h->match = match ? 1 : 0;
+  h->max_batch = max_batch;
+  h->ldb = (max_batch + kChunk - 1) / kChunk * kChunk;
+  auto bail = [&](int rc) { ibl_ib_destroy(h); return rc; };
+  int rc;
+  const size_t inbox = (size_t)g->n_e * h->ldb;
+  if ((rc = dalloc(&h->cin, inbox)) || (rc = dalloc(&h->vin, inbox)) || (rc = dalloc(&h->ch8, (size_t)g->n_v * h->ldb)) ||
+      (rc = dalloc(&h->flags, (size_t)imax * kShards)) || (rc = dalloc(&h->dL, 1)))
+    return bail(rc);
+  if (hipMemset(h->cin, 0, inbox) != hipSuccess || hipMemset(h->vin, 0, inbox) != hipSuccess ||
+      hipMemset(h->ch8, 0, (size_t)g->n_v * h->ldb) != hipSuccess || hipMemset(h->flags, 0, sizeof(int32_t) * imax * kShards) != hipSuccess)
+    return bail(fail(IBL_EHIP, "hipMemset failed"));
+
+  const std::vector<int> cdeg = present(g->h_cn_deg), vdeg = present(g->h_vn_deg);
+  const bool deg_ok = CM <= kMaxD && VM <= kMaxD;
+  const int cn_nraw = h->match ? CM - 3 : CM - 2;
+  int cn_nt = cn_nraw, vn_nraw = h->match ? std::max(VM - 2, 0) : VM - 1, vn_nt = vn_nraw;
+  if (h->match) {
+    cn_nt += (int)cdeg.size();
+    for (int d : vdeg) vn_nt += (d >= 2);
+  }
+  const int max_nt = kLdsBytes / kTbl;
+  h->fast = !(flags & IBL_FLAG_FORCE_GENERIC) && Tc == T && T <= kTP && deg_ok && cn_nt <= max_nt &&
+            vn_nt <= max_nt && VM <= max_nt && cn_nt > 0;
+
+  if (h->fast) {
+    // ---------------- CN images: pass p = 0 (iteration 0 ops) .. imax-1
+    std::vector<uint32_t> cimg, vimg, dimg;
+    const int64_t T2 = (int64_t)T * T;
+    auto cn_raw = [&](int p, int l, int t, int m) -> int {
+      int64_t idx;
+      if (p == 0) idx = (l == 0) ? (int64_t)t * Tc + m : (int64_t)Tc * Tc + (int64_t)(l - 1) * Tc * T + (int64_t)t * T + m;
+      else idx = (int64_t)Tc * Tc + (int64_t)(CM - 3) * Tc * T + (int64_t)(p - 1) * (CM - 2) * T2 + l * T2 + (int64_t)t * T + m;
+      return cn_lut[idx];
+    };
+    for (int p = 0; p < imax; ++p) {
+      for (int l = 0; l < cn_nraw; ++l) append(cimg, make_table(T, [&](int t, int m) { return cn_raw(p, l, t, m); }));
+      int slot = cn_nraw;
+      for (int d : cdeg) {
+        if (!h->match) {
+          h->cn_fslot[d] = d >= 3 ? d - 3 : 0;
+          continue;
+        }
+        const int64_t mrow = (int64_t)p * T * CM + (int64_t)(d - 1) * T;
+        if (d == 2) append(cimg, make_table(T, [&](int t, int) { return match_cn[mrow + t]; }));
+        else append(cimg, make_table(T, [&](int t, int m) { return match_cn[mrow + cn_raw(p, d - 3, t, m)]; }));
+        h->cn_fslot[d] = slot++;
+      }
+    }
+    h->cn_nt = cn_nt;
+    // ---------------- VN images: pass k = 0 .. imax-2 (extrinsic), decision images k = 0 .. imax-1
+    auto vn_raw = [&](int k, int l, int t, int m) -> int {
+      const int64_t off = (int64_t)k * ((int64_t)Tc * T + (int64_t)(VM - 1) * T2);
+      const int64_t idx = off + (l == 0 ? (int64_t)t * T + m : (int64_t)Tc * T + (int64_t)(l - 1) * T2 + (int64_t)t * T + m);
+      return vn_lut[idx];
+    };
+    for (int k = 0; k < std::max(imax - 1, 1); ++k) {
+      for (int l = 0; l < vn_nraw; ++l) append(vimg, make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
+      int slot = vn_nraw;
+      for (int d : vdeg) {
+        if (d < 2) continue;
+        if (!h->match) {
+          h->vn_fslot[d] = d - 2;
+          continue;
+        }
+        const int64_t mrow = (int64_t)k * T * VM + (int64_t)(d - 1) * T;
+        append(vimg, make_table(T, [&](int t, int m) { return match_vn[mrow + vn_raw(k, d - 2, t, m)]; }));
+        h->vn_fslot[d] = slot++;
+      }
+    }
+    h->vn_nt = vn_nt;
+    for (int k = 0; k < imax; ++k)
+      for (int l = 0; l < VM; ++l) append(dimg, make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
+    h->dec_nt = VM;
+    if ((rc = dupload(&h->cn_img, cimg.data(), cimg.size())) || (rc = dupload(&h->vn_img, vimg.data(), vimg.size())) ||
+        (rc = dupload(&h->dec_img, dimg.data(), dimg.size())))
+      return bail(rc);
+    if ((rc = pick_cfg(0, CM, h->cn_nt, g->num_cus, &h->kcn)) || (rc = pick_cfg(1, VM, std::max(h->vn_nt, 1), g->num_cus, &h->kvn)) ||
+        (rc = pick_cfg(2, VM, h->dec_nt, g->num_cus, &h->kdec)))
+      return bail(rc);
+  } else {
+    h->cn_len = cn_len; h->vn_len = vn_len;
+    if ((rc = dupload(&h->cn_lut, cn_lut, cn_len)) || (rc = dupload(&h->vn_lut, vn_lut, vn_len))) return bail(rc);
+    if (h->match) {
+      h->mc_len = mc_len; h->mv_len = mv_len;
+      if ((rc = dupload(&h->mc, match_cn, mc_len)) || (rc = dupload(&h->mv, match_vn, mv_len))) return bail(rc);
+    }
+  }
+  *out = h;
+  return IBL_OK;
+}
+
+int ibl_ib_path(const ibl_ib* h) { return h && h->fast ? 1 : 0; }
+
+int ibl_ib_timing(ibl_ib* h, int32_t enable) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  h->timer.on = enable != 0;
+  return IBL_OK;
+}
+int ibl_ib_timing_read(ibl_ib* h, double* cn_ms, int32_t* cn_n, double* vn_ms, int32_t* vn_n) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  return h->timer.read(cn_ms, cn_n, vn_ms, vn_n) ? fail(IBL_EHIP, "event timing failed") : IBL_OK;
+}
+int ibl_float_timing(ibl_float* h, int32_t enable) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  h->timer.on = enable != 0;
+  return IBL_OK;
+}
+int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_n, double* vn_ms, int32_t* vn_n) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  return h->timer.read(cn_ms, cn_n, vn_ms, vn_n) ? fail(IBL_EHIP, "event timing failed") : IBL_OK;
+}
+
+void ibl_ib_destroy(ibl_ib* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->g->device);
+  dfree(h->cin); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
+  dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img);
+  dfree(h->cn_lut); dfree(h->vn_lut); dfree(h->mc); dfree(h->mv);
+  delete h;
+}
+
+int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void* d_out, int32_t out_dtype,
+                  int32_t early_stop, int32_t* d_iters, void* stream) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (B < 1 || B > h->max_batch) return fail(IBL_EINVAL, "B must lie in [1, max_batch]");
+  if (ch_dtype != kU8 && ch_dtype != kI32) return fail(IBL_EINVAL, "channel dtype must be IBL_U8 or IBL_I32");
+  if (out_dtype != kU8 && out_dtype != kI32) return fail(IBL_EINVAL, "output dtype must be IBL_U8 or IBL_I32");
+  if (!d_ch || !d_out) return fail(IBL_EINVAL, "NULL buffer");
+  const ibl_graph* g = h->g;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(g->device));
+  const int I = h->imax;
+  const bool early = early_stop != 0 && I > 1;
+  if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
+  HIPCHK(launch_ib_stage(d_ch, ch_dtype, g->n_v, B, h->ch8, h->ldb, s));
+  const int nchunks = (B + kChunk - 1) / kChunk;
+  if (h->fast) {
+    IbFastArgs cn{}, vn{};
+    cn.ch8 = vn.ch8 = h->ch8;
+    cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin;
+    vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
+    cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.nchunks = vn.nchunks = nchunks;
+    cn.ldb = vn.ldb = h->ldb;
+    cn.B = vn.B = B;
+    cn.half = vn.half = h->T / 2;
+    cn.match = vn.match = h->match;
+    cn.nt = h->cn_nt; vn.nt = h->vn_nt;
+    std::memcpy(cn.fslot, h->cn_fslot, sizeof(cn.fslot));
+    std::memcpy(vn.fslot, h->vn_fslot, sizeof(vn.fslot));
+    // pass 0: send + checknode_update_iter0, inputs gathered from the staged channel rows
+    cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));
+    cn.in = h->cin; cn.gather = nullptr;
+    for (int j = 1; j < I; ++j) {
+      const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+      vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 64;
+      vn.gate = gate;
+      HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_fast(vn, h->VM, h->kvn.grid, h->kvn.block, h->kvn.lds, s); }));
+      cn.img = h->cn_img + (size_t)j * h->cn_nt * 64;
+      cn.gate = gate;
+      cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));
+    }
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    IbDecArgs dc{};
+    dc.vin = h->vin; dc.ch8 = h->ch8; dc.start = g->vn_start; dc.deg = g->vn_deg; dc.img = h->dec_img;
+    dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.nt = h->dec_nt; dc.n_nodes = g->n_v;
+    dc.nchunks = nchunks; dc.ldb = h->ldb; dc.B = B;
+    const size_t esz = out_dtype == kU8 ? 1 : 4;
+    dc.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
+    HIPCHK(launch_ib_dec_fast(dc, h->kdec.grid, h->kdec.block, h->kdec.lds, s));
+  } else {
+    IbGenArgs cn{}, vn{};
+    cn.ch8 = vn.ch8 = h->ch8;
+    cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin; cn.lut = h->cn_lut;
+    cn.lut_len = h->cn_len; cn.mt = h->mc; cn.mt_len = h->mc_len;
+    vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin; vn.lut = h->vn_lut;
+    vn.lut_len = h->vn_len; vn.mt = h->mv; vn.mt_len = h->mv_len;
+    cn.Tc = vn.Tc = h->Tc; cn.T = vn.T = h->T; cn.CM = vn.CM = h->CM; cn.VM = vn.VM = h->VM;
+    cn.match = vn.match = h->match;
+    cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.ldb = vn.ldb = h->ldb; cn.B = vn.B = B; cn.half = vn.half = h->T / 2;
+    cn.pass = 0; cn.in = nullptr; cn.gather = g->csr_cols;
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_gen(cn, s); }));
+    cn.in = h->cin; cn.gather = nullptr;
+    for (int j = 1; j < I; ++j) {
+      const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+      vn.pass = j - 1; vn.gate = gate;
+      HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_gen(vn, s); }));
+      cn.pass = j; cn.gate = gate; cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_gen(cn, s); }));
+    }
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    IbGenDecArgs dc{};
+    dc.vin = h->vin; dc.ch8 = h->ch8; dc.start = g->vn_start; dc.deg = g->vn_deg; dc.lut = h->vn_lut;
+    dc.lut_len = h->vn_len; dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.Tc = h->Tc; dc.T = h->T;
+    dc.VM = h->VM; dc.n_nodes = g->n_v; dc.ldb = h->ldb; dc.B = B;
+    HIPCHK(launch_ib_dec_gen(dc, s));
+  }
+  return IBL_OK;
+}
+
+// ------------------------------------------------------------------ float decoder
+int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_max, int32_t precision,
+                     int32_t max_batch, ibl_float** out) {
+  if (!out) return fail(IBL_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!g) return fail(IBL_EINVAL, "graph is NULL");
+  if (kind != IBL_MINSUM && kind != IBL_BP) return fail(IBL_EINVAL, "kind must be IBL_MINSUM or IBL_BP");
+  if (precision != kF32 && precision != kF64) return fail(IBL_EINVAL, "precision must be IBL_F32 or IBL_F64");
+  if (imax < 1 || max_batch < 1) return fail(IBL_EINVAL, "imax and max_batch must be >= 1");
+  if (g->dcm > kMaxD || g->dvm > kMaxD) return fail(IBL_EUNSUPPORTED, "float decoders support node degrees <= 16");
+  HIPCHK(hipSetDevice(g->device));
+  auto* h = new ibl_float();
+  h->g = g; h->kind = kind; h->imax = imax; h->prec = precision; h->max_batch = max_batch; h->llr_max = llr_max;
+  h->ldb = (max_batch + kChunk - 1) / kChunk * kChunk;
+  const size_t es = precision == kF32 ? 4 : 8;
+  const size_t inbox = (size_t)g->n_e * h->ldb * es;
+  int rc;
+  auto bail = [&](int r) { ibl_float_destroy(h); return r; };
+  uint8_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+  if ((rc = dalloc(&a, inbox)) || (rc = dalloc(&b, inbox)) || (rc = dalloc(&c, inbox)) ||
+      (rc = dalloc(&d, (size_t)g->n_v * h->ldb * es)) || (rc = dalloc(&h->flags, (size_t)imax * kShards)) ||
+      (rc = dalloc(&h->dL, 1))) {
+    dfree(a); dfree(b); dfree(c); dfree(d);
+    return bail(rc);
+  }
+  h->cin = a; h->vbuf0 = b; h->vbuf1 = c; h->chf = d;
+  if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess)
+    return bail(fail(IBL_EHIP, "hipMemset failed"));
+  int bpc = 0;
+  if (fl_occupancy(0, kind, precision, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  h->grid_cn = bpc * g->num_cus;
+  if (fl_occupancy(1, kind, precision, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  h->grid_vn = bpc * g->num_cus;
+  *out = h;
+  return IBL_OK;
+}
+
+void ibl_float_destroy(ibl_float* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->g->device);
+  dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
+  delete h;
+}
+
+int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out, int32_t out_dtype,
+                     int32_t early_stop, int32_t* d_iters, void* stream) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (B < 1 || B > h->max_batch) return fail(IBL_EINVAL, "B must lie in [1, max_batch]");
+  if ((llr_dtype != kF32 && llr_dtype != kF64) || (out_dtype != kF32 && out_dtype != kF64))
+    return fail(IBL_EINVAL, "LLR dtypes must be IBL_F32 or IBL_F64");
+  if (!d_llr || !d_out) return fail(IBL_EINVAL, "NULL buffer");
+  const ibl_graph* g = h->g;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(g->device));
+  const int I = h->imax;
+  const bool early = early_stop != 0 && I > 1;
+  const int cwl = h->prec == kF32 ? 4 : 2;
+  const int nchunks = (B + 64 * cwl - 1) / (64 * cwl);
+  if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
+  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, s));
+  FlArgs send{};
+  send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
+  send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;
+  HIPCHK(launch_fl_send(send, h->prec, s));
+  FlArgs cn{}, vn{};
+  cn.in = h->cin; cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn;
+  vn.out = h->cin; vn.ch = h->chf; vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn;
+  cn.llr_max = vn.llr_max = h->llr_max;
+  cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+  cn.nchunks = vn.nchunks = nchunks;
+  cn.ldb = vn.ldb = h->ldb;
+  cn.B = vn.B = B;
+  for (int j = 1; j < I; ++j) {
+    void* vb = (j & 1) ? h->vbuf1 : h->vbuf0;
+    cn.out = vb;
+    cn.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
+    cn.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn(cn, h->kind, h->prec, h->grid_cn, s); }));
+    vn.in = vb;
+    vn.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+    HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn(vn, h->prec, h->grid_vn, s); }));
+  }
+  HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+  FlDecArgs dc{};
+  dc.vin0 = h->vbuf0; dc.vin1 = h->vbuf1; dc.ch = h->chf; dc.start = g->vn_start; dc.deg = g->vn_deg;
+  dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.n_nodes = g->n_v; dc.nchunks = nchunks;
+  dc.ldb = h->ldb; dc.B = B;
+  const size_t total = (size_t)g->n_v * B;
+  HIPCHK(launch_fl_dec(dc, h->prec, (int)std::min<size_t>((total + 255) / 256, 8192), s));
+  return IBL_OK;
+}
+
+int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
+                    int64_t* d_count, void* stream) {
+  if (!d_x || !d_count) return fail(IBL_EINVAL, "NULL buffer");
+  if (dtype < kU8 || dtype > kF64) return fail(IBL_EINVAL, "bad dtype");
+  if (rows < 0 || B < 0 || ld < B) return fail(IBL_EINVAL, "bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(d_count, 0, sizeof(int64_t), s));
+  if (rows == 0 || B == 0) return IBL_OK;
+  HIPCHK(launch_count_below(d_x, dtype, rows, B, ld, threshold, reinterpret_cast<unsigned long long*>(d_count), s));
+  return IBL_OK;
+}
+
+}  // extern "C"

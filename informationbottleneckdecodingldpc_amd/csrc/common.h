@@ -1,0 +1,129 @@
+// Shared definitions for the MI355X (gfx950) LDPC decoding kernels.
+//
+// Message layout: every inbox is [edge][codeword] with a padded row stride `ldb`
+// (codeword-minor, like the reference's inbox buffers, discrete_LDPC_decoder_irreg.py:214-219),
+// so the lanes of a wavefront touch consecutive codewords of one edge row: one 256-B (u8) or
+// 1-KiB (fp32) coalesced segment per row and wave.  A "wave item" is one node × one chunk of
+// kChunk codewords.
+#pragma once
+#include <hip/hip_runtime.h>
+#pragma clang diagnostic ignored "-Wunused-result"
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ibl {
+
+constexpr int kWave = 64;
+constexpr int kChunk = 256;       // codewords per wave item (u8: 4 per lane, fp32: 4, fp64: 2x2)
+constexpr int kTbl = 8192;        // one IB lookup table replicated over the 32 LDS banks
+constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
+constexpr int kMaxD = 16;         // largest node degree with an unrolled fast-path body
+constexpr int kShards = 64;       // early-stop flag words per iteration (one wave load)
+constexpr int kLdsBytes = 160 * 1024;
+
+enum Dtype : int32_t { kU8 = 1, kI32 = 2, kF32 = 3, kF64 = 4 };
+
+// ---------------------------------------------------------------- IB fast path
+struct IbFastArgs {
+  const uint8_t* in;        // own-order inbox (nullptr for CN pass 0: inputs gathered from ch8)
+  uint8_t* out;             // other-order inbox
+  const uint8_t* ch8;       // staged channel cluster ids [N][ldb]
+  const int32_t* start;     // node -> first own-order edge
+  const int32_t* deg;       // node degree
+  const int32_t* tgt;       // own-order edge -> other-order row
+  const int32_t* gather;    // CN pass 0: csr_cols (edge -> variable node); else nullptr
+  const uint32_t* img;      // this pass's tables: nt x 64 dwords (256 entries, t*16+m)
+  const int32_t* gate;      // kShards flag words that must be non-zero to run (nullptr: run)
+  int32_t* unsat;           // kShards flag words to set when a check is unsatisfied (nullptr: no syndrome)
+  int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
+  int32_t nt;               // tables staged in LDS
+  int32_t n_nodes, nchunks, ldb, B, half, match;
+};
+
+struct IbDecArgs {
+  const uint8_t* vin;       // varnode_inbox [E][ldb]
+  const uint8_t* ch8;
+  const int32_t* start;
+  const int32_t* deg;
+  const uint32_t* img;      // decision tables for every pass: imax x nt x 64 dwords
+  const int32_t* iters;     // device scalar L (pass index of the decision tables)
+  void* out;                // user output [N][B]
+  int32_t out_dtype, nt, n_nodes, nchunks, ldb, B, aligned;
+};
+
+// --------------------------------------------------------------- IB generic path
+// Reference-exact flat-vector indexing (any T_ch, T_dec <= 256, any degree).
+struct IbGenArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  const uint8_t* ch8;
+  const int32_t* start;
+  const int32_t* deg;
+  const int32_t* tgt;
+  const int32_t* gather;
+  const int32_t* lut;       // flat int32 CN or VN vector
+  const int32_t* mt;        // flat matching vector
+  const int32_t* gate;
+  int32_t* unsat;
+  int64_t lut_len, mt_len;
+  int32_t pass, Tc, T, CM, VM, match, n_nodes, ldb, B, half;
+};
+
+struct IbGenDecArgs {
+  const uint8_t* vin;
+  const uint8_t* ch8;
+  const int32_t* start;
+  const int32_t* deg;
+  const int32_t* lut;
+  const int32_t* iters;
+  void* out;
+  int64_t lut_len;
+  int32_t out_dtype, Tc, T, VM, n_nodes, ldb, B;
+};
+
+// ------------------------------------------------------------------- float path
+struct FlArgs {
+  const void* in;           // own-order inbox (F)
+  void* out;                // other-order inbox (F)
+  const void* ch;           // staged channel LLRs [N][ldb] (F)
+  const int32_t* start;
+  const int32_t* deg;
+  const int32_t* tgt;
+  const int32_t* gate;
+  int32_t* unsat;
+  double llr_max;
+  int32_t n_nodes, nchunks, ldb, B;
+};
+
+struct FlDecArgs {
+  const void* vin0;         // ping-pong varnode inboxes, selected by parity of L
+  const void* vin1;
+  const void* ch;
+  const int32_t* start;
+  const int32_t* deg;
+  const int32_t* iters;
+  void* out;
+  int32_t out_dtype, n_nodes, nchunks, ldb, B, aligned;
+};
+
+// launchers (defined in the .hip translation units, called by capi.hip)
+hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb, hipStream_t s);
+hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
+hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
+hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
+hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu);
+hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
+hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
+hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);
+hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s);
+hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
+                              unsigned long long* cnt, hipStream_t s);
+
+hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s);
+hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s);
+hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int grid, hipStream_t s);
+hipError_t launch_fl_vn(const FlArgs& a, int prec, int grid, hipStream_t s);
+hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
+hipError_t fl_occupancy(int which, int kind, int prec, int* blocks_per_cu);
+
+}  // namespace ibl

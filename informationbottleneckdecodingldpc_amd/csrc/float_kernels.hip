@@ -1,0 +1,340 @@
+// Float min-sum / belief-propagation LDPC decoding kernels for MI355X (gfx950).
+//
+// Replaces Continous_LDPC_Decoding/kernels_min_and_BP.cl (fp64 in the reference):
+//   send_channel_values_to_checknode_inbox -> fl_stage + fl_cn (first pass gathers nothing: the
+//                                            staged channel rows are scattered by fl_send)
+//   checknode_update_minsum (:126-167)    -> fl_cn<MINSUM>
+//   checknode_update + boxplus (:5-71)    -> fl_cn<BP>
+//   varnode_update (:76-123)              -> fl_vn
+//   calc_syndrome (:206-227)              -> fused into fl_cn (parity of its inputs)
+//   calc_varnode_output (:170-204)        -> fl_dec
+//
+// Precision: F = float (the BASELINE's float32 build) or double (strict parity build).
+//   * min-sum is computed from (min1, min2, sign product, zero count) of the node's inputs —
+//     bit-identical to the reference's sequential sign/min fold, which only selects values;
+//   * BP folds are evaluated with prefix sharing in exactly the reference's per-output order
+//     (t = boxplus(m_next, t), clamped at every step); fp64 uses the reference's formula
+//     log((1+e^{a+b})/(e^a+e^b)), fp32 the overflow-free equivalent
+//     sgn(a)sgn(b)min(|a|,|b|) + log1p(e^-|a+b|) - log1p(e^-|a-b|) (the naive form overflows
+//     float for a+b > 88);
+//   * variable-node sums keep the reference's addition order (channel first, then ascending
+//     edges) through prefix sharing, so fp64 sums are bit-identical.
+// Each wave item is one node x kChunk codewords; a lane holds 16 bytes of every edge row
+// (4 fp32 or 2 fp64 codewords; fp64 items cover 128 codewords).
+#include <algorithm>
+
+#include "common.h"
+
+namespace ibl {
+
+template <typename F> struct Vec;
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  using T = float4;
+  __device__ static float get(const T& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
+  __device__ static void set(T& v, int s, float x) {
+    if (s == 0) v.x = x; else if (s == 1) v.y = x; else if (s == 2) v.z = x; else v.w = x;
+  }
+};
+template <> struct Vec<double> {
+  static constexpr int N = 2;
+  using T = double2;
+  __device__ static double get(const T& v, int s) { return s == 0 ? v.x : v.y; }
+  __device__ static void set(T& v, int s, double x) { if (s == 0) v.x = x; else v.y = x; }
+};
+
+template <typename F> __device__ __forceinline__ F ocl_sign(F x) {
+  return x > F(0) ? F(1) : (x < F(0) ? F(-1) : (x != x ? F(0) : x));
+}
+// sign(t) * min(llr_max, sign(t) * t)  (kernels_min_and_BP.cl:69,120)
+template <typename F> __device__ __forceinline__ F clampllr(F t, F lm) {
+  const F s = ocl_sign(t);
+  const F a = s * t;
+  return s * ((a < lm) ? a : lm);
+}
+
+__device__ __forceinline__ double boxplus(double a, double b, double lm) {
+  const double boxp = log((1.0 + exp(a + b)) / (exp(a) + exp(b)));
+  return clampllr(boxp, lm);
+}
+__device__ __forceinline__ float boxplus(float a, float b, float lm) {
+  const float s = ((a < 0.f) != (b < 0.f)) ? -1.f : 1.f;
+  const float mn = fminf(fabsf(a), fabsf(b));
+  float r = s * mn + __logf(1.f + __expf(-fabsf(a + b))) - __logf(1.f + __expf(-fabsf(a - b)));
+  if (a == 0.f || b == 0.f) r = 0.f;
+  return clampllr(r, lm);
+}
+
+__device__ __forceinline__ bool fl_gate(const int32_t* gate, int lane) {
+  if (!gate) return true;
+  return __ballot(gate[lane] != 0) != 0ull;
+}
+
+template <int KIND, typename F, int D>
+__device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, bool do_par, int valid, bool& unsat) {
+  using V = Vec<F>;
+  typename V::T in[D], out[D];
+  const F* src = reinterpret_cast<const F*>(a.in);
+  F* dst = reinterpret_cast<F*>(a.out);
+  const F lm = (F)a.llr_max;
+#pragma unroll
+  for (int j = 0; j < D; ++j) in[j] = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
+#pragma unroll
+  for (int s = 0; s < V::N; ++s) {
+    F m[D], o[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) m[j] = V::get(in[j], s);
+    if (do_par && s < valid) {
+      bool p = false;
+#pragma unroll
+      for (int j = 0; j < D; ++j) p ^= (m[j] < F(0));
+      unsat |= p;
+    }
+    if constexpr (KIND == 0) {
+      // min-sum (kernels_min_and_BP.cl:156-162): |out_w| = min over the others, sign = product
+      F mn1 = F(INFINITY), mn2 = F(INFINITY);
+      int idx = -1, nz = 0;
+      bool neg = false;
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        const F x = m[j] < F(0) ? -m[j] : m[j];
+        if (x < mn1) { mn2 = mn1; mn1 = x; idx = j; } else if (x < mn2) { mn2 = x; }
+        neg ^= (m[j] < F(0));
+        nz += (m[j] == F(0));
+      }
+#pragma unroll
+      for (int w = 0; w < D; ++w) {
+        const F mag = (w == idx) ? mn2 : mn1;
+        const bool zw = (m[w] == F(0));
+        const bool ng = neg ^ (m[w] < F(0));
+        o[w] = (nz - (zw ? 1 : 0)) > 0 ? F(0) : (ng ? -mag : mag);
+      }
+    } else {
+      // BP sequential box-plus folds with prefix sharing (kernels_min_and_BP.cl:63-69)
+      F t = m[1];
+#pragma unroll
+      for (int j = 2; j < D; ++j) t = boxplus(m[j], t, lm);
+      o[0] = clampllr(t, lm);
+      F P = m[0];
+#pragma unroll
+      for (int w = 1; w <= D - 2; ++w) {
+        t = P;
+#pragma unroll
+        for (int j = w + 1; j < D; ++j) t = boxplus(m[j], t, lm);
+        o[w] = clampllr(t, lm);
+        P = boxplus(m[w], P, lm);
+      }
+      o[D - 1] = clampllr(P, lm);
+    }
+#pragma unroll
+    for (int w = 0; w < D; ++w) V::set(out[w], s, o[w]);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w)
+    *reinterpret_cast<typename V::T*>(dst + (size_t)a.tgt[st + w] * a.ldb + cw0) = out[w];
+}
+
+template <typename F, int D>
+__device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, int cw0) {
+  using V = Vec<F>;
+  typename V::T in[D], out[D];
+  const F* src = reinterpret_cast<const F*>(a.in);
+  F* dst = reinterpret_cast<F*>(a.out);
+  const F lm = (F)a.llr_max;
+  const typename V::T cv = *reinterpret_cast<const typename V::T*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
+#pragma unroll
+  for (int j = 0; j < D; ++j) in[j] = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
+#pragma unroll
+  for (int s = 0; s < V::N; ++s) {
+    const F c = V::get(cv, s);
+    F m[D], o[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) m[j] = V::get(in[j], s);
+    if constexpr (D == 1) {
+      o[0] = clampllr(c, lm);
+    } else {
+      // t = ch + others in ascending order (kernels_min_and_BP.cl:113-118)
+      F t = c + m[1];
+#pragma unroll
+      for (int j = 2; j < D; ++j) t = t + m[j];
+      o[0] = clampllr(t, lm);
+      F Q = c + m[0];
+#pragma unroll
+      for (int w = 1; w <= D - 2; ++w) {
+        t = Q;
+#pragma unroll
+        for (int j = w + 1; j < D; ++j) t = t + m[j];
+        o[w] = clampllr(t, lm);
+        Q = Q + m[w];
+      }
+      o[D - 1] = clampllr(Q, lm);
+    }
+#pragma unroll
+    for (int w = 0; w < D; ++w) V::set(out[w], s, o[w]);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w)
+    *reinterpret_cast<typename V::T*>(dst + (size_t)a.tgt[st + w] * a.ldb + cw0) = out[w];
+}
+
+#define FL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+
+template <int KIND, typename F>
+__global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
+  const int lane = threadIdx.x & 63;
+  if (!fl_gate(a.gate, lane)) return;
+  constexpr int CWL = Vec<F>::N;
+  constexpr int CH = 64 * CWL;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int nitems = a.n_nodes * a.nchunks;
+  const bool do_par = a.unsat != nullptr;
+  bool unsat = false;
+  for (int item = gw; item < nitems; item += nw) {
+    const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+    const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+    const int d = a.deg[node], st = a.start[node];
+    const int cw0 = chunk * CH + lane * CWL;
+    const int valid = a.B - cw0;
+    switch (d) {
+#define X(D) case D: fl_cn_item<KIND, F, D>(a, st, cw0, do_par, valid, unsat); break;
+      FL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  }
+  if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
+}
+
+template <typename F>
+__global__ __launch_bounds__(256) void fl_vn(FlArgs a) {
+  const int lane = threadIdx.x & 63;
+  if (!fl_gate(a.gate, lane)) return;
+  constexpr int CWL = Vec<F>::N;
+  constexpr int CH = 64 * CWL;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int nitems = a.n_nodes * a.nchunks;
+  for (int item = gw; item < nitems; item += nw) {
+    const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+    const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+    const int d = a.deg[node], st = a.start[node];
+    const int cw0 = chunk * CH + lane * CWL;
+    switch (d) {
+      case 1: fl_vn_item<F, 1>(a, node, st, cw0); break;
+#define X(D) case D: fl_vn_item<F, D>(a, node, st, cw0); break;
+      FL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  }
+}
+
+// APP LLR = ch + sum of all inputs in ascending order, unclamped (kernels_min_and_BP.cl:196-202)
+template <typename F>
+__global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
+  const int L = __builtin_amdgcn_readfirstlane(*a.iters);
+  const F* vin = reinterpret_cast<const F*>((L & 1) ? a.vin1 : a.vin0);
+  const F* ch = reinterpret_cast<const F*>(a.ch);
+  const size_t total = (size_t)a.n_nodes * a.B;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i / a.B);
+    const int b = (int)(i - (size_t)n * a.B);
+    const int d = a.deg[n], st = a.start[n];
+    F x = ch[(size_t)n * a.ldb + b];
+    if (L > 0)
+      for (int v = 0; v < d; ++v) x = x + vin[(size_t)(st + v) * a.ldb + b];
+    if (a.out_dtype == kF32) reinterpret_cast<float*>(a.out)[i] = (float)x;
+    else reinterpret_cast<double*>(a.out)[i] = (double)x;
+  }
+}
+
+// channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded
+template <typename F>
+__global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb) {
+  const size_t total = (size_t)n * ldb;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / ldb);
+    const int b = (int)(i - (size_t)row * ldb);
+    F v = F(0);
+    if (b < B) {
+      const size_t k = (size_t)row * B + b;
+      v = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
+    }
+    dst[i] = v;
+  }
+}
+
+// send_channel_values_to_checknode_inbox (kernels_min_and_BP.cl:12-29): scatter staged rows
+template <typename F>
+__global__ void fl_send(FlArgs a) {
+  const F* ch = reinterpret_cast<const F*>(a.ch);
+  F* dst = reinterpret_cast<F*>(a.out);
+  const int per = a.ldb / 4;
+  const size_t total = (size_t)a.n_nodes * per;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i / per);
+    const int b4 = (int)(i - (size_t)n * per) * 4;
+    if (b4 >= a.B) continue;
+    const int d = a.deg[n], st = a.start[n];
+    F v[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) v[s] = ch[(size_t)n * a.ldb + b4 + s];
+    for (int w = 0; w < d; ++w) {
+      F* p = dst + (size_t)a.tgt[st + w] * a.ldb + b4;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) p[s] = v[s];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------- launchers
+hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s) {
+  const size_t total = (size_t)n * ldb;
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  if (prec == kF32) hipLaunchKernelGGL(fl_stage<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (float*)dst, ldb);
+  else hipLaunchKernelGGL(fl_stage<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (double*)dst, ldb);
+  return hipGetLastError();
+}
+
+hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s) {
+  const size_t total = (size_t)a.n_nodes * (a.ldb / 4);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  if (prec == kF32) hipLaunchKernelGGL(fl_send<float>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fl_send<double>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int grid, hipStream_t s) {
+  if (prec == kF32) {
+    if (kind == 0) hipLaunchKernelGGL((fl_cn<0, float>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fl_cn<1, float>), dim3(grid), dim3(256), 0, s, a);
+  } else {
+    if (kind == 0) hipLaunchKernelGGL((fl_cn<0, double>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((fl_cn<1, double>), dim3(grid), dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fl_vn(const FlArgs& a, int prec, int grid, hipStream_t s) {
+  if (prec == kF32) hipLaunchKernelGGL(fl_vn<float>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fl_vn<double>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
+  if (prec == kF32) hipLaunchKernelGGL(fl_dec<float>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(fl_dec<double>, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t fl_occupancy(int which, int kind, int prec, int* blocks_per_cu) {
+  const void* f;
+  if (which == 0) {
+    f = prec == kF32 ? (kind == 0 ? (const void*)fl_cn<0, float> : (const void*)fl_cn<1, float>)
+                     : (kind == 0 ? (const void*)fl_cn<0, double> : (const void*)fl_cn<1, double>);
+  } else {
+    f = prec == kF32 ? (const void*)fl_vn<float> : (const void*)fl_vn<double>;
+  }
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
+}
+
+}  // namespace ibl

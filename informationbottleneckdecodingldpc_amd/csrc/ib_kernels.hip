@@ -1,0 +1,586 @@
+// Information-bottleneck (integer lookup-table) LDPC decoding kernels for MI355X (gfx950).
+//
+// Replaces the reference's OpenCL kernels Discrete_LDPC_decoding/kernels_template_irreg.cl
+// (and the regular copy kernels_template.cl):
+//   checknode_update_iter0 + send_channel_values_to_checknode_inbox  -> ib_cn_fast (pass 0)
+//   checknode_update + calc_syndrome + host stop test                -> ib_cn_fast (pass p>=1)
+//   varnode_update                                                   -> ib_vn_fast
+//   calc_varnode_output                                              -> ib_dec_fast
+//
+// Fast path design (T_ch == T_dec <= 16, degrees <= kMaxD):
+//   * messages are u8, [edge][codeword]; a wave item = one node x 256 codewords, 4 codewords
+//     per lane packed in one dword per edge row (coalesced 256-B row segments);
+//   * the pass's lookup tables are staged in LDS, each 16x16 table replicated over the 32
+//     banks (entry e=(t,m) in LDS row e>>2, bank = lane&31, byte e&3), so every ds_read_u8
+//     lookup is bank-conflict free and costs one v_lshl_add (row of t) + one DS op;
+//   * the order-sensitive folds are computed with prefix sharing (bit-exact: same ops in the
+//     same order as the reference's per-output folds, kernels_template_irreg.cl:205-231),
+//     25 instead of 35 lookups for a degree-7 check, 35 instead of 56 for a degree-8 variable;
+//   * the matching step (MATCH, :84-91/:162-172/:233-240) is pre-composed on the host into
+//     the final fold table of each degree, so it costs no lookup;
+//   * the syndrome of the batch-global early stop (:304-326 + decoder :310-320) is fused
+//     into the check-node pass (parity of its inputs), and published as device flags that
+//     gate the next launches — no host readback inside the iteration loop.
+#include <algorithm>
+
+#include "common.h"
+
+namespace ibl {
+
+__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
+  return ((m >> 2) << 7) + (m & 3u) + lane4;
+}
+
+__device__ __forceinline__ uint32_t valid_mask4(int remaining) {
+  return remaining >= 4 ? 0xFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
+}
+
+__device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
+  if (!gate) return true;
+  return __ballot(gate[lane] != 0) != 0ull;
+}
+
+__device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nt) {
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+  const int n = nt * (kTbl / 4);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
+}
+
+// A wave item's inputs, fetched one item ahead of its computation (register double buffer):
+// the row loads of item k+1 are issued before item k is computed, so HBM latency overlaps the
+// lookups and the waits never cover the previous item's stores.
+template <int MAXD>
+struct ItemBuf {
+  uint32_t row[MAXD];   // 4 packed u8 messages (codewords cw0..cw0+3) of each input row
+  uint32_t tg[MAXD];    // destination row of each output edge (tgt[st + j]), fetched with the rows
+  uint32_t chw;         // channel values (VN) of the same 4 codewords
+  int d, st, node;
+  uint32_t cw0;
+};
+
+template <int MAXD, bool VN, bool GATHER>
+__device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, ItemBuf<MAXD>& b) {
+  const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+  const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+  b.node = node;
+  b.d = a.deg[node];
+  b.st = a.start[node];
+  b.cw0 = (uint32_t)(chunk * kChunk + lane * 4);
+  // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
+  // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
+#pragma unroll
+  for (int j = 0; j < MAXD; ++j) {
+    const int e = b.st + min(j, b.d - 1);
+    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
+    b.row[j] = *reinterpret_cast<const uint32_t*>(row + b.cw0);
+  }
+  if (VN) b.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + b.cw0);
+  // the output-edge targets travel in the same in-order vector-memory stream as the rows (an
+  // opaque zero keeps them off the scalar path, whose waits would also drain the LDS lookups)
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+  for (int j = 0; j < MAXD; ++j) b.tg[j] = (uint32_t)a.tgt[b.st + min(j, b.d - 1) + z];
+}
+
+__device__ __forceinline__ uint32_t pack4(const uint32_t (&t)[4]) {
+  return t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
+}
+
+// ------------------------------------------------------------------ check node
+// Inputs in_0..in_{D-1} (CN order = ascending column). Output w is the left fold over the
+// other inputs with table l at fold step l (kernels_template_irreg.cl:226-231):
+//   out[0]   = fold(in_1, in_2, ...),   out[w] = fold(P_w, in_{w+1}, ...),  P_w = fold(in_0..in_{w-1})
+// Step l uses LDS slot l, except the last step (l = D-3) which uses fslot (matching composed).
+// The 4 codewords of a lane are advanced together so each fold step issues 4 independent reads.
+template <int D, int MAXD>
+__device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
+                                           const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
+  uint32_t outw[D];
+  const uint32_t fbase = (uint32_t)fslot * kTbl;
+  if (do_par) {
+    uint32_t par = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint32_t p = 0;
+#pragma unroll
+      for (int j = 0; j < D; ++j) p ^= (__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8) < (uint32_t)a.half) ? 1u : 0u;
+      par |= p << s;
+    }
+    if (par & valid_mask4(a.B - (int)b.cw0)) unsat = true;
+  }
+  if constexpr (D == 2) {
+    if (a.match) {
+      uint32_t t0[4], t1[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        t0[s] = lds[(__builtin_amdgcn_ubfe(b.row[1], 8 * s, 8) << 9) + lane4 + fbase];
+        t1[s] = lds[(__builtin_amdgcn_ubfe(b.row[0], 8 * s, 8) << 9) + lane4 + fbase];
+      }
+      outw[0] = pack4(t0);
+      outw[1] = pack4(t1);
+    } else {
+      outw[0] = b.row[1];
+      outw[1] = b.row[0];
+    }
+  } else {
+    uint32_t q[D][4];
+#pragma unroll
+    for (int j = 1; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) q[j][s] = qidx(__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8), lane4);
+    auto sb = [&](int l) -> uint32_t { return (l == D - 3) ? fbase : (uint32_t)(l * kTbl); };
+    uint32_t t[4], P[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) t[s] = __builtin_amdgcn_ubfe(b.row[1], 8 * s, 8);
+#pragma unroll
+    for (int j = 2; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+    outw[0] = pack4(t);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) P[s] = __builtin_amdgcn_ubfe(b.row[0], 8 * s, 8);
+#pragma unroll
+    for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = P[s];
+#pragma unroll
+      for (int j = w + 1; j < D; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+      outw[w] = pack4(t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
+    }
+    outw[D - 1] = pack4(P);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w)
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)b.tg[w] * a.ldb + b.cw0) = outw[w];
+}
+
+// ---------------------------------------------------------------- variable node
+// Inputs: channel c and in_0..in_{D-1} (VN order = ascending row). Extrinsic output w folds
+// c and the other inputs (kernels_template_irreg.cl:151-160): step 0 = channel table V_0,
+// step l = V_l; the last step (l = D-2) uses fslot (matching composed). Degree 1 forwards c
+// (:131-136).
+template <int D, int MAXD>
+__device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
+                                           const ItemBuf<MAXD>& b, int fslot) {
+  uint32_t outw[D];
+  if constexpr (D == 1) {
+    outw[0] = b.chw;
+  } else {
+    const uint32_t fbase = (uint32_t)fslot * kTbl;
+    auto sb = [&](int l) -> uint32_t { return (l == D - 2) ? fbase : (uint32_t)(l * kTbl); };
+    uint32_t q[D][4], c[4], t[4], Q[4];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) q[j][s] = qidx(__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8), lane4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c[s] = __builtin_amdgcn_ubfe(b.chw, 8 * s, 8) << 9;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
+#pragma unroll
+    for (int j = 2; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+    outw[0] = pack4(t);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
+#pragma unroll
+    for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = Q[s];
+#pragma unroll
+      for (int j = w + 1; j < D; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+      outw[w] = pack4(t);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+    }
+    outw[D - 1] = pack4(Q);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w)
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)b.tg[w] * a.ldb + b.cw0) = outw[w];
+}
+
+// ------------------------------------------------------------- decision output
+// calc_varnode_output (kernels_template_irreg.cl:279-300): fold of channel and ALL inputs with
+// the raw tables V_0..V_{D-1} of pass L, no matching.
+__device__ __forceinline__ void store4(void* out, int dtype, size_t row_off, int cw0, int B, bool aligned,
+                                       uint32_t packed) {
+  if (dtype == kU8) {
+    uint8_t* p = reinterpret_cast<uint8_t*>(out) + row_off + cw0;
+    if (aligned && cw0 + 4 <= B) {
+      *reinterpret_cast<uint32_t*>(p) = packed;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (cw0 + s < B) p[s] = (uint8_t)(packed >> (8 * s));
+    }
+  } else {
+    int32_t* p = reinterpret_cast<int32_t*>(out) + row_off + cw0;
+    if (aligned && cw0 + 4 <= B) {
+      int4 v = make_int4(packed & 0xff, (packed >> 8) & 0xff, (packed >> 16) & 0xff, packed >> 24);
+      *reinterpret_cast<int4*>(p) = v;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (cw0 + s < B) p[s] = (int32_t)((packed >> (8 * s)) & 0xff);
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds, uint32_t lane4, int node,
+                                         int st, uint32_t cw0) {
+  uint32_t inw[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) inw[j] = *reinterpret_cast<const uint32_t*>(a.vin + (size_t)(st + j) * a.ldb + cw0);
+  const uint32_t cw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + cw0);
+  uint32_t packed = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t c = __builtin_amdgcn_ubfe(cw, 8 * s, 8);
+    uint32_t Q = lds[(c << 9) + qidx(__builtin_amdgcn_ubfe(inw[0], 8 * s, 8), lane4)];
+#pragma unroll
+    for (int k = 1; k < D; ++k)
+      Q = lds[(Q << 9) + qidx(__builtin_amdgcn_ubfe(inw[k], 8 * s, 8), lane4) + k * kTbl];
+    packed |= Q << (8 * s);
+  }
+  store4(a.out, a.out_dtype, (size_t)node * a.B, (int)cw0, a.B, a.aligned != 0, packed);
+}
+
+// ---------------------------------------------------------------------- kernels
+#define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
+#define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+
+// Persistent wave loop shared by the CN and VN passes: items (node, 256-codeword chunk) are dealt
+// round-robin to the grid's waves; each iteration prefetches the next item, then computes the
+// current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch).
+template <int MAXD, bool VN, bool GATHER>
+__device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const int wpb = blockDim.x >> 6;
+  const int gw = blockIdx.x * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
+  const int nitems = a.n_nodes * a.nchunks;
+  const bool do_par = !VN && a.unsat != nullptr;
+  bool unsat = false;
+  auto compute = [&](const ItemBuf<MAXD>& cur) {
+    if constexpr (VN) {
+      switch (cur.d) {
+        case 1: vn_compute<1, MAXD>(a, lds, lane4, cur, 0); break;
+#define X(D) case D: if constexpr (D <= MAXD) vn_compute<D, MAXD>(a, lds, lane4, cur, a.fslot[D]); break;
+        IBL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+    } else {
+      switch (cur.d) {
+#define X(D) case D: if constexpr (D <= MAXD) cn_compute<D, MAXD>(a, lds, lane4, cur, a.fslot[D], do_par, unsat); break;
+        IBL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+    }
+  };
+  // ping-pong buffers (no register copies: a copy would wait for the prefetched loads)
+  ItemBuf<MAXD> A, Bb;
+  int item = gw;
+  if (item < nitems) fetch_item<MAXD, VN, GATHER>(a, item, lane, A);
+  while (item < nitems) {
+    int next = item + nw;
+    if (next < nitems) fetch_item<MAXD, VN, GATHER>(a, next, lane, Bb);
+    compute(A);
+    item = next;
+    if (item >= nitems) break;
+    next = item + nw;
+    if (next < nitems) fetch_item<MAXD, VN, GATHER>(a, next, lane, A);
+    compute(Bb);
+    item = next;
+  }
+  if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
+}
+
+template <int MAXD, bool GATHER>
+__global__ __launch_bounds__(1024) void ib_cn_fast(IbFastArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
+  stage_tables(lds, a.img, a.nt);
+  __syncthreads();
+  ib_pass<MAXD, false, GATHER>(a, lds);
+}
+
+template <int MAXD>
+__global__ __launch_bounds__(1024) void ib_vn_fast(IbFastArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (!gate_open(a.gate, threadIdx.x & 63)) return;
+  stage_tables(lds, a.img, a.nt);
+  __syncthreads();
+  ib_pass<MAXD, true, false>(a, lds);
+}
+
+__global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int L = __builtin_amdgcn_readfirstlane(*a.iters);
+  stage_tables(lds, a.img + (size_t)L * a.nt * 64, a.nt);
+  __syncthreads();
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const int wpb = blockDim.x >> 6;
+  const int gw = blockIdx.x * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
+  const int nitems = a.n_nodes * a.nchunks;
+  for (int item = gw; item < nitems; item += nw) {
+    const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+    const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+    const int d = a.deg[node], st = a.start[node];
+    const uint32_t cw0 = (uint32_t)(chunk * kChunk + lane * 4);
+    if ((int)cw0 >= a.B) continue;
+    switch (d) {
+      case 1: dec_item<1>(a, lds, lane4, node, st, cw0); break;
+#define X(D) case D: dec_item<D>(a, lds, lane4, node, st, cw0); break;
+      IBL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  }
+}
+
+// ------------------------------------------------------ channel staging (u8 / i32 -> u8)
+__global__ void ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb) {
+  const int quads = ldb >> 2;
+  const size_t total = (size_t)n * quads;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / quads);
+    const int cw0 = (int)(i - (size_t)row * quads) * 4;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cw = cw0 + s;
+      uint32_t v = 0;
+      if (cw < B) {
+        if (dtype == kU8) {
+          v = reinterpret_cast<const uint8_t*>(ch)[(size_t)row * B + cw];
+        } else {
+          const int32_t x = reinterpret_cast<const int32_t*>(ch)[(size_t)row * B + cw];
+          v = (uint32_t)min(max(x, 0), 255);
+        }
+      }
+      packed |= v << (8 * s);
+    }
+    *reinterpret_cast<uint32_t*>(ch8 + (size_t)row * ldb + cw0) = packed;
+  }
+}
+
+// ----------------------------------------------------------------- generic IB path
+// One thread per (node, codeword); reference-exact flat LUT indexing (index clamped to the
+// vector so malformed input cannot fault). Used when T_ch != T_dec, T_dec > 16 or a node
+// degree exceeds kMaxD.
+__device__ __forceinline__ int32_t lut_at(const int32_t* lut, int64_t len, int64_t idx) {
+  idx = idx < 0 ? 0 : (idx >= len ? len - 1 : idx);
+  return lut[idx];
+}
+
+__device__ __forceinline__ uint32_t gen_msg(const IbGenArgs& a, int e, int b) {
+  return a.gather ? a.ch8[(size_t)a.gather[e] * a.ldb + b] : a.in[(size_t)e * a.ldb + b];
+}
+
+__global__ void ib_cn_gen(IbGenArgs a) {
+  const int lane = threadIdx.x & 63;
+  if (!gate_open(a.gate, lane)) return;
+  const int nb = (a.B + blockDim.x - 1) / blockDim.x;
+  bool unsat = false;
+  for (int it = blockIdx.x; it < a.n_nodes * nb; it += gridDim.x) {
+    const int c = it / nb;
+    const int b = (it - c * nb) * blockDim.x + threadIdx.x;
+    if (b >= a.B) continue;
+    const int d = a.deg[c], st = a.start[c];
+    if (a.unsat) {
+      uint32_t p = 0;
+      for (int w = 0; w < d; ++w) p ^= gen_msg(a, st + w, b) < (uint32_t)a.half;
+      unsat |= p != 0;
+    }
+    const int64_t T = a.T, Tc = a.Tc;
+    const int64_t off = Tc * Tc + (int64_t)(a.CM - 3) * Tc * T + (int64_t)(a.pass - 1) * (a.CM - 2) * T * T;
+    for (int w = 0; w < d; ++w) {
+      auto other = [&](int pos) -> int64_t { return gen_msg(a, st + (pos < w ? pos : pos + 1), b); };
+      int64_t x;
+      if (a.pass == 0) {
+        if (d >= 3) {
+          x = lut_at(a.lut, a.lut_len, other(0) * Tc + other(1));
+          for (int l = 1; l < d - 2; ++l)
+            x = lut_at(a.lut, a.lut_len, x * T + other(l + 1) + Tc * Tc + (int64_t)(l - 1) * Tc * T);
+        } else {
+          x = other(0);
+        }
+      } else {
+        x = other(0);
+        for (int l = 0; l < d - 2; ++l) x = lut_at(a.lut, a.lut_len, off + x * T + other(l + 1) + (int64_t)l * T * T);
+      }
+      if (a.match) x = lut_at(a.mt, a.mt_len, (int64_t)a.pass * T * a.CM + (int64_t)(d - 1) * T + x);
+      a.out[(size_t)a.tgt[st + w] * a.ldb + b] = (uint8_t)x;
+    }
+  }
+  if (a.unsat && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[blockIdx.x & (kShards - 1)], 1);
+}
+
+__global__ void ib_vn_gen(IbGenArgs a) {
+  const int lane = threadIdx.x & 63;
+  if (!gate_open(a.gate, lane)) return;
+  const int nb = (a.B + blockDim.x - 1) / blockDim.x;
+  const int64_t T = a.T, Tc = a.Tc;
+  const int64_t off = (int64_t)a.pass * (Tc * T + (int64_t)(a.VM - 1) * T * T);
+  for (int it = blockIdx.x; it < a.n_nodes * nb; it += gridDim.x) {
+    const int n = it / nb;
+    const int b = (it - n * nb) * blockDim.x + threadIdx.x;
+    if (b >= a.B) continue;
+    const int d = a.deg[n], st = a.start[n];
+    const int64_t c = a.ch8[(size_t)n * a.ldb + b];
+    if (d == 1) {
+      a.out[(size_t)a.tgt[st] * a.ldb + b] = (uint8_t)c;
+      continue;
+    }
+    for (int w = 0; w < d; ++w) {
+      auto other = [&](int pos) -> int64_t { return a.in[(size_t)(st + (pos < w ? pos : pos + 1)) * a.ldb + b]; };
+      int64_t x = lut_at(a.lut, a.lut_len, off + c * T + other(0));
+      for (int l = 1; l <= d - 2; ++l)
+        x = lut_at(a.lut, a.lut_len, off + x * T + other(l) + Tc * T + (int64_t)(l - 1) * T * T);
+      if (a.match) x = lut_at(a.mt, a.mt_len, (int64_t)a.pass * T * a.VM + (int64_t)(d - 1) * T + x);
+      a.out[(size_t)a.tgt[st + w] * a.ldb + b] = (uint8_t)x;
+    }
+  }
+}
+
+__global__ void ib_dec_gen(IbGenDecArgs a) {
+  const int nb = (a.B + blockDim.x - 1) / blockDim.x;
+  const int L = *a.iters;
+  const int64_t T = a.T, Tc = a.Tc;
+  const int64_t off = (int64_t)L * (Tc * T + (int64_t)(a.VM - 1) * T * T);
+  for (int it = blockIdx.x; it < a.n_nodes * nb; it += gridDim.x) {
+    const int n = it / nb;
+    const int b = (it - n * nb) * blockDim.x + threadIdx.x;
+    if (b >= a.B) continue;
+    const int d = a.deg[n], st = a.start[n];
+    const int64_t c = a.ch8[(size_t)n * a.ldb + b];
+    int64_t x = lut_at(a.lut, a.lut_len, off + c * T + a.vin[(size_t)st * a.ldb + b]);
+    for (int l = 1; l < d; ++l)
+      x = lut_at(a.lut, a.lut_len, off + x * T + a.vin[(size_t)(st + l) * a.ldb + b] + Tc * T + (int64_t)(l - 1) * T * T);
+    if (a.out_dtype == kU8) reinterpret_cast<uint8_t*>(a.out)[(size_t)n * a.B + b] = (uint8_t)x;
+    else reinterpret_cast<int32_t*>(a.out)[(size_t)n * a.B + b] = (int32_t)x;
+  }
+}
+
+// --------------------------------------------------- stop iteration + error counter
+// L = first loop iteration j in [1, imax-1] whose flags are all zero (syndrome satisfied),
+// else imax-1: the i_num-1 of decode_OpenCL (discrete_LDPC_decoder_irreg.py:277-333).
+__global__ void finalize_iters(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user) {
+  const int lane = threadIdx.x & 63;
+  int L = imax - 1;
+  if (early) {
+    for (int j = 1; j <= imax - 1; ++j) {
+      if (__ballot(flags[(size_t)j * kShards + lane] != 0) == 0ull) {
+        L = j;
+        break;
+      }
+    }
+  }
+  if (lane == 0) {
+    *dL = L;
+    if (user) *user = L;
+  }
+}
+
+__global__ void count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
+                            unsigned long long* cnt) {
+  unsigned long long c = 0;
+  const int64_t total = rows * (int64_t)B;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / B, b = i - r * B;
+    const int64_t k = r * ld + b;
+    double v;
+    switch (dtype) {
+      case kU8: v = reinterpret_cast<const uint8_t*>(x)[k]; break;
+      case kI32: v = reinterpret_cast<const int32_t*>(x)[k]; break;
+      case kF32: v = reinterpret_cast<const float*>(x)[k]; break;
+      default: v = reinterpret_cast<const double*>(x)[k]; break;
+    }
+    c += (v < thr) ? 1ull : 0ull;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+// -------------------------------------------------------------------- launchers
+hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb, hipStream_t s) {
+  const size_t total = (size_t)n * (ldb / 4);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(ib_stage, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, ch8, ldb);
+  return hipGetLastError();
+}
+hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
+  if (a.gather) {
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, true>), dim3(grid), dim3(block), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_fast<16, true>), dim3(grid), dim3(block), lds, s, a);
+  } else {
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, false>), dim3(grid), dim3(block), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_fast<16, false>), dim3(grid), dim3(block), lds, s, a);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
+  if (maxd <= 8) hipLaunchKernelGGL(ib_vn_fast<8>, dim3(grid), dim3(block), lds, s, a);
+  else hipLaunchKernelGGL(ib_vn_fast<16>, dim3(grid), dim3(block), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(ib_dec_fast, dim3(grid), dim3(block), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu) {
+  if (which == 0) {  // both variants must accept the LDS size; report the non-gather one
+    for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>}) {
+      hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+  }
+  const void* f = which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
+                : which == 1 ? (maxd <= 8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>)
+                             : (const void*)ib_dec_fast;
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, block, lds);
+}
+static int gen_grid(int n_nodes, int B) {
+  const long long items = (long long)n_nodes * ((B + 255) / 256);
+  return (int)std::min<long long>(items, 65536);
+}
+hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ib_cn_gen, dim3(gen_grid(a.n_nodes, a.B)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ib_vn_gen, dim3(gen_grid(a.n_nodes, a.B)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ib_dec_gen, dim3(gen_grid(a.n_nodes, a.B)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_iters, dim3(1), dim3(64), 0, s, flags, imax, early, dL, user);
+  return hipGetLastError();
+}
+hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
+                              unsigned long long* cnt, hipStream_t s) {
+  const int64_t total = rows * (int64_t)B;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
+  hipLaunchKernelGGL(count_below, dim3(grid), dim3(256), 0, s, x, dtype, rows, B, ld, thr, cnt);
+  return hipGetLastError();
+}
+
+}  // namespace ibl

@@ -1,0 +1,190 @@
+"""Device-side decoder objects over the C ABI (torch tensors as device memory, HIP streams).
+
+These are the building blocks of the reference-compatible classes
+(:mod:`.discrete_LDPC_decoder`, :mod:`.discrete_LDPC_decoder_irreg`,
+:mod:`.min_sum_decoder_irreg`, :mod:`.bp_decoder_irreg`). PyTorch is only plumbing:
+allocation, streams and ``torch.distributed``; every decode runs the HIP kernels of
+``libibldpc.so`` and there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .graph import EdgeGraph, build_graph
+from .tables import IBTables
+
+_DT_IB = {torch.uint8: _lib.IBL_U8, torch.int32: _lib.IBL_I32}
+_DT_FL = {torch.float32: _lib.IBL_F32, torch.float64: _lib.IBL_F64}
+_DT_ANY = {torch.uint8: _lib.IBL_U8, torch.int32: _lib.IBL_I32, torch.float32: _lib.IBL_F32,
+           torch.float64: _lib.IBL_F64}
+
+
+def _require_gpu(device) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("no HIP device visible: the LDPC decoders run only on the GPU (no CPU fallback)")
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"decoder device must be a HIP (cuda) device, got {dev}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def _stream_ptr(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _check_tensor(t: torch.Tensor, dev: torch.device, n_rows: int, name: str) -> None:
+    if not isinstance(t, torch.Tensor) or t.device != dev:
+        raise ValueError(f"{name} must be a tensor on {dev}")
+    if t.dim() != 2 or t.shape[0] != n_rows or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous [{n_rows}][B] tensor, got {tuple(t.shape)}")
+
+
+class Graph:
+    """A code graph uploaded to one device (``ibl_graph``)."""
+
+    def __init__(self, H_or_graph, device=None):
+        self.device = _require_gpu(device)
+        self.edges: EdgeGraph = H_or_graph if isinstance(H_or_graph, EdgeGraph) else build_graph(H_or_graph)
+        g = self.edges
+        L = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(L.ibl_graph_create(g.n_v, g.n_c, np.ascontiguousarray(g.csr_indptr, np.int32),
+                                      np.ascontiguousarray(g.csr_cols, np.int32), self.device.index,
+                                      ctypes.byref(h)), "ibl_graph_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().ibl_graph_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+
+class IBDecoder:
+    """Information-bottleneck lookup-table decoder (``ibl_ib``) for up to ``max_batch`` codewords."""
+
+    def __init__(self, graph: Graph, tables: IBTables, match: bool, max_batch: int, force_generic: bool = False):
+        self.graph = graph
+        self.tables = tables
+        self.match = bool(match)
+        self.max_batch = int(max_batch)
+        self.device = graph.device
+        tb = tables
+        cn = np.ascontiguousarray(tb.cn, np.int32)
+        vn = np.ascontiguousarray(tb.vn, np.int32)
+        mc = np.ascontiguousarray(tb.match_cn if tb.match_cn is not None else np.zeros(1), np.int32)
+        mv = np.ascontiguousarray(tb.match_vn if tb.match_vn is not None else np.zeros(1), np.int32)
+        h = ctypes.c_void_p()
+        L = _lib.load()
+        _lib.check(L.ibl_ib_create(graph.handle, tb.Tc, tb.T, tb.imax, cn, cn.size, vn, vn.size, mc, mc.size,
+                                   mv, mv.size, int(self.match), self.max_batch,
+                                   _lib.IBL_FLAG_FORCE_GENERIC if force_generic else 0, ctypes.byref(h)),
+                   "ibl_ib_create")
+        self._h = h
+        self.fast_path = bool(L.ibl_ib_path(h))
+
+    def decode(self, ch: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=torch.int32,
+               early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Decode ``ch`` ([N][B] cluster ids, uint8/int32, on the decoder's device)."""
+        n = self.graph.edges.n_v
+        _check_tensor(ch, self.device, n, "channel values")
+        if ch.dtype not in _DT_IB:
+            raise ValueError("channel values must be uint8 or int32")
+        B = ch.shape[1]
+        if out is None:
+            out = torch.empty((n, B), dtype=out_dtype, device=self.device)
+        _check_tensor(out, self.device, n, "output")
+        if out.dtype not in _DT_IB or out.shape[1] != B:
+            raise ValueError("output must be uint8/int32 [N][B]")
+        it_ptr = None
+        if iters is not None:
+            if iters.dtype != torch.int32 or iters.device != self.device or iters.numel() < 1:
+                raise ValueError("iters must be an int32 device tensor")
+            it_ptr = iters.data_ptr()
+        _lib.check(_lib.load().ibl_ib_decode(self._h, ch.data_ptr(), _DT_IB[ch.dtype], B, out.data_ptr(),
+                                             _DT_IB[out.dtype], int(bool(early_stop)), it_ptr,
+                                             _stream_ptr(self.device)), "ibl_ib_decode")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().ibl_ib_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+
+class FloatDecoder:
+    """Float min-sum (kind=0) / BP (kind=1) decoder (``ibl_float``); precision fp32 or fp64."""
+
+    def __init__(self, graph: Graph, kind: int, imax: int, max_batch: int, precision=torch.float32,
+                 llr_max: float = 150.0):
+        self.graph = graph
+        self.kind = int(kind)
+        self.imax = int(imax)
+        self.max_batch = int(max_batch)
+        self.precision = precision
+        self.device = graph.device
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().ibl_float_create(graph.handle, self.kind, self.imax, float(llr_max),
+                                                _DT_FL[precision], self.max_batch, ctypes.byref(h)),
+                   "ibl_float_create")
+        self._h = h
+
+    def decode(self, llr: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=None,
+               early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
+        n = self.graph.edges.n_v
+        _check_tensor(llr, self.device, n, "channel LLRs")
+        if llr.dtype not in _DT_FL:
+            raise ValueError("channel LLRs must be float32 or float64")
+        B = llr.shape[1]
+        if out is None:
+            out = torch.empty((n, B), dtype=out_dtype or self.precision, device=self.device)
+        _check_tensor(out, self.device, n, "output")
+        if out.dtype not in _DT_FL or out.shape[1] != B:
+            raise ValueError("output must be float32/float64 [N][B]")
+        it_ptr = iters.data_ptr() if iters is not None else None
+        _lib.check(_lib.load().ibl_float_decode(self._h, llr.data_ptr(), _DT_FL[llr.dtype], B, out.data_ptr(),
+                                                _DT_FL[out.dtype], int(bool(early_stop)), it_ptr,
+                                                _stream_ptr(self.device)), "ibl_float_decode")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().ibl_float_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+
+def count_below(x: torch.Tensor, rows: int, threshold: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device count of ``x[:rows] < threshold`` (the reference's error counters) -> int64 tensor."""
+    if x.dim() != 2 or not x.is_contiguous() or x.device.type != "cuda":
+        raise ValueError("x must be a contiguous 2-D device tensor")
+    if x.dtype not in _DT_ANY:
+        raise ValueError("unsupported dtype")
+    if out is None:
+        out = torch.empty(1, dtype=torch.int64, device=x.device)
+    rows = min(int(rows), x.shape[0])
+    _lib.check(_lib.load().ibl_count_below(x.data_ptr(), _DT_ANY[x.dtype], rows, x.shape[1], x.shape[1],
+                                           float(threshold), out.data_ptr(), _stream_ptr(x.device)),
+               "ibl_count_below")
+    return out

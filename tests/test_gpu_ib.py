@@ -1,0 +1,187 @@
+"""GPU parity of the information-bottleneck decoder (HIP kernels via the C ABI) against the CPU
+oracle (oracle/ib_oracle.c, itself pinned to the reference's decode_on_host by
+tests/test_cpu_oracle.py) and against the reference's own golden outputs.
+
+Bar: bit-exact cluster ids and identical stop iteration.
+"""
+import numpy as np
+import pytest
+import torch
+
+from informationbottleneckdecodingldpc_amd import codes, graph, tables
+from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from informationbottleneckdecodingldpc_amd import engine
+    return engine
+
+
+def _run(eng, g_edges, tb, ch, match, early, out_dtype=torch.int32, ch_dtype=torch.int32, force_generic=False,
+         graph_obj=None):
+    G = graph_obj or eng.Graph(g_edges, DEV)
+    dec = eng.IBDecoder(G, tb, match, max_batch=ch.shape[1], force_generic=force_generic)
+    it = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = dec.decode(torch.from_numpy(ch).to(DEV).to(ch_dtype).contiguous(), out_dtype=out_dtype,
+                     early_stop=early, iters=it)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().astype(np.int32), int(it.item()), dec
+
+
+CASES = [
+    # name, imax, B, match, early
+    ("wlan", 1, 3, False, False),
+    ("wlan", 2, 5, True, False),
+    ("wlan", 10, 300, True, False),
+    ("wlan", 10, 257, False, True),
+    ("reg", 6, 64, False, False),
+    ("reg", 5, 511, True, True),
+    ("dvb", 4, 6, True, False),
+    ("dvb", 3, 2, False, True),
+]
+
+
+def _code(name, wlan_H, reg_H, dvb_H):
+    return {"wlan": wlan_H, "reg": reg_H, "dvb": dvb_H}[name]
+
+
+@pytest.mark.parametrize("name,imax,B,match,early", CASES)
+@pytest.mark.parametrize("generic", [False, True])
+def test_ib_random_tables_vs_oracle(eng, name, imax, B, match, early, generic, wlan_H, reg_H, dvb_H):
+    g = graph.build_graph(_code(name, wlan_H, reg_H, dvb_H))
+    T = 16
+    tb = tables.random_tables(T, T, g.d_c_max, g.d_v_max, imax, seed=imax * 7 + B)
+    rng = np.random.default_rng(B)
+    ch = rng.integers(0, T, (g.n_v, B)).astype(np.int32)
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
+    out, it, dec = _run(eng, g, tb, ch, match, early, force_generic=generic)
+    assert dec.fast_path == (not generic)
+    assert it == ref_it
+    np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("ch_dtype,out_dtype", [(torch.uint8, torch.uint8), (torch.uint8, torch.int32),
+                                                (torch.int32, torch.uint8)])
+@pytest.mark.parametrize("B", [1, 4, 7, 256, 1030])
+def test_ib_dtypes_and_ragged_batches(eng, wlan_H, ch_dtype, out_dtype, B):
+    g = graph.build_graph(wlan_H)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 4, seed=5)
+    ch = np.random.default_rng(B).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=True)
+    out, _, _ = _run(eng, g, tb, ch, True, False, out_dtype=out_dtype, ch_dtype=ch_dtype)
+    np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("Tc,T", [(16, 8), (8, 8), (4, 16), (32, 32)])
+def test_ib_other_alphabets(eng, reg_H, Tc, T):
+    """T_ch != T_dec and T_dec > 16 run the generic path; T == T_ch <= 16 the fast path."""
+    g = graph.build_graph(reg_H)
+    imax = 4
+    tb = tables.random_tables(Tc, T, g.d_c_max, g.d_v_max, imax, seed=Tc + T)
+    ch = np.random.default_rng(1).integers(0, Tc, (g.n_v, 37)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=True)
+    out, _, dec = _run(eng, g, tb, ch, True, False)
+    assert dec.fast_path == (Tc == T and T <= 16)
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_ib_early_stop_converging(eng, wlan_H):
+    """LLR-quantised tables at good SNR: the batch converges before imax; same stop iteration and
+    outputs as the oracle, with matching on."""
+    g = graph.build_graph(wlan_H)
+    q = UniformQuantizer(sigma2_from_ebn0(4.0, g.R_c), 16)
+    imax = 30
+    tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
+    ch = q.sample_all_zero(g.n_v, 40, np.random.default_rng(3))
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=True, early_stop=True, return_iters=True)
+    out, it, _ = _run(eng, g, tb, ch, True, True)
+    assert ref_it < imax - 1
+    assert it == ref_it
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_reference_golden_decode_on_host(golden, reg_H, wlan_H):
+    """Drop-in decode_on_host (HIP kernels) == the reference's decode_on_host outputs."""
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder import Discrete_LDPC_Decoder_class
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+        Discrete_LDPC_Decoder_class_irregular
+    z = golden
+    for imax in (1, 2, 10):
+        dec = Discrete_LDPC_Decoder_class(reg_H, imax, 16, 16, z[f"reg_imax{imax}_cn"], z[f"reg_imax{imax}_vn"], 4)
+        for k in range(3):
+            out = dec.decode_on_host(z[f"reg_imax{imax}_ch"][:, k])
+            np.testing.assert_array_equal(out, z[f"reg_imax{imax}_out"][:, k])
+        deci = Discrete_LDPC_Decoder_class_irregular(wlan_H, imax, 16, 16, z[f"wlan_imax{imax}_cn"],
+                                                     z[f"wlan_imax{imax}_vn"], None, None, 4, match="true")
+        for k in range(3):
+            out = deci.decode_on_host(z[f"wlan_imax{imax}_ch"][:, k])
+            np.testing.assert_array_equal(out, z[f"wlan_imax{imax}_out"][:, k].astype(np.float64))
+
+
+def test_dropin_decode_opencl_and_errors(wlan_H):
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+        Discrete_LDPC_Decoder_class_irregular
+    g = graph.build_graph(wlan_H)
+    imax = 8
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=11)
+    B = 100
+    dec = Discrete_LDPC_Decoder_class_irregular(wlan_H, imax, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
+                                                match="true")
+    dec.init_OpenCL_decoding(B, 0)
+    ch = np.random.default_rng(0).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    host_out = dec.decode_OpenCL(ch)                       # numpy in, numpy out
+    ref = oracle.ib_decode(g, tb, ch, match=True, early_stop=True)
+    np.testing.assert_array_equal(host_out, ref)
+    buf = dec.decode_OpenCL(torch.from_numpy(ch).to(DEV), buffer_in=True, return_buffer=True)
+    assert isinstance(buf, torch.Tensor) and buf.device.type == "cuda"
+    np.testing.assert_array_equal(buf.cpu().numpy(), ref)
+    assert dec.return_errors_all_zero(buf) == int((ref[:dec.data_len] < 8).sum())
+    assert dec.data_len == 648
+
+
+def test_full_size_dvbs2_properties(eng, dvb_H):
+    """BASELINE size (DVB-S2 N=64800, B=8192, imax=50, match on): deterministic, shard-equivalent
+    (1 batch == 2 half batches), and spot columns equal the oracle."""
+    g = graph.build_graph(dvb_H)
+    imax, B = 50, 8192
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=2)
+    G = eng.Graph(g, DEV)
+    dec = eng.IBDecoder(G, tb, True, B)
+    assert dec.fast_path
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(0)
+    ch = torch.randint(0, 16, (g.n_v, B), device=DEV, dtype=torch.uint8, generator=gen)
+    o1 = dec.decode(ch, out_dtype=torch.uint8, early_stop=False).clone()
+    o2 = dec.decode(ch, out_dtype=torch.uint8, early_stop=False).clone()
+    assert torch.equal(o1, o2)
+    h1 = dec.decode(ch[:, :B // 2].contiguous(), out_dtype=torch.uint8, early_stop=False).clone()
+    h2 = dec.decode(ch[:, B // 2:].contiguous(), out_dtype=torch.uint8, early_stop=False).clone()
+    assert torch.equal(torch.cat([h1, h2], 1), o1)
+    cols = [0, 1, 4095, 8191]
+    ref = oracle.ib_decode(g, tb, ch[:, cols].cpu().numpy().astype(np.int32), match=True)
+    np.testing.assert_array_equal(o1[:, cols].cpu().numpy().astype(np.int32), ref)
+
+
+def test_full_size_dvbs2_decodes_all_zero(eng, dvb_H):
+    """LLR-quantised tables at 3 dB: every one of 8192 all-zero codewords decodes (0 errors).
+    (No early stop happens here: the degree-1 parity bit forwards its channel value unchanged,
+    kernels_template_irreg.cl:131-136, so ~8 % of codewords keep one unsatisfied check and the
+    batch-global syndrome never reaches zero.)"""
+    g = graph.build_graph(dvb_H)
+    q = UniformQuantizer(sigma2_from_ebn0(3.0, g.R_c), 16)
+    imax, B = 50, 8192
+    tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
+    dec = eng.IBDecoder(eng.Graph(g, DEV), tb, True, B)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(1)
+    ch = q.sample_all_zero_device(g.n_v, B, DEV, generator=gen)
+    it = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = dec.decode(ch, out_dtype=torch.uint8, early_stop=True, iters=it)
+    errs = int(eng.count_below(out, g.data_len, 8).item())
+    assert errs == 0

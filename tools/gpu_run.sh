@@ -1,0 +1,38 @@
+#!/bin/bash
+# GPU-box session: tests, bench, rocprofv3 kernel trace. Stops at the first crash-like exit.
+# usage: bash tools/gpu_run.sh <tag> [tests|bench|prof|pmc ...]
+set -u
+TAG=${1:-run}; shift
+STEPS=${@:-tests bench prof}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+crash() { case $1 in 124|134|137|139) echo "crash-like exit $1 in $2, stopping" | tee -a $O/summary.txt; exit $1;; esac; }
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest $R/tests -m gpu -q --timeout 400 -p no:cacheprovider > $O/pytest.log 2>&1
+      rc=$?; echo "pytest rc=$rc $(tail -1 $O/pytest.log)" >> $O/summary.txt; crash $rc pytest;;
+    smoke)
+      timeout -k 10 300 python -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc" >> $O/summary.txt; crash $rc smoke;;
+    bench)
+      timeout -k 10 400 python $R/bench.py > $O/bench.json 2> $O/bench.err
+      rc=$?; echo "bench rc=$rc" >> $O/summary.txt; crash $rc bench;;
+    benchfloat)
+      for k in minsum bp; do
+        timeout -k 10 400 python $R/bench.py --kind $k --no-cpu-baseline --steps 3 > $O/bench_$k.json 2> $O/bench_$k.err
+        rc=$?; echo "bench $k rc=$rc" >> $O/summary.txt; crash $rc bench_$k
+      done;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 3 > $O/bench_prof.json 2> $O/prof.err)
+      rc=$?; echo "rocprof rc=$rc" >> $O/summary.txt; crash $rc rocprof;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/bench_pmc_$c.json 2> $O/pmc_$c.err)
+        rc=$?; echo "pmc $c rc=$rc" >> $O/summary.txt; crash $rc pmc_$c
+      done;;
+  esac
+done
+echo done >> $O/summary.txt
