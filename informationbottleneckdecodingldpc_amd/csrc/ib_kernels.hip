@@ -27,6 +27,12 @@
 
 namespace ibl {
 
+// Read-only graph arrays read through the constant address space: uniform indices become scalar
+// loads (the compiler cannot otherwise prove they do not alias the inbox being written, and would
+// issue vector loads whose waits drain every outstanding row load).
+typedef __attribute__((address_space(4))) const int32_t cint32;
+__device__ __forceinline__ int32_t sload(const int32_t* p, int i) { return ((cint32*)p)[i]; }
+
 __device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
   return ((m >> 2) << 7) + (m & 3u) + lane4;
 }
@@ -52,7 +58,7 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
 template <int MAXD>
 struct ItemBuf {
   uint32_t row[MAXD];   // 4 packed u8 messages (codewords cw0..cw0+3) of each input row
-  uint32_t tg[MAXD];    // destination row of each output edge (tgt[st + j]), fetched with the rows
+  uint32_t tgv;         // lane j < d holds the destination row tgt[st + j] of output edge j
   uint32_t chw;         // channel values (VN) of the same 4 codewords
   int d, st, node;
   uint32_t cw0;
@@ -63,24 +69,32 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
   const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
   b.node = node;
-  b.d = a.deg[node];
-  b.st = a.start[node];
+  b.d = sload(a.deg, node);
+  b.st = sload(a.start, node);
   b.cw0 = (uint32_t)(chunk * kChunk + lane * 4);
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
-    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
+    const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
     b.row[j] = *reinterpret_cast<const uint32_t*>(row + b.cw0);
   }
   if (VN) b.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + b.cw0);
-  // the output-edge targets travel in the same in-order vector-memory stream as the rows (an
-  // opaque zero keeps them off the scalar path, whose waits would also drain the LDS lookups)
-  int z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  else b.chw = 0;
+  // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
+  // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
+  b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
+}
+
+// Empty asm that consumes every register of a fetched item: the compiler inserts ONE counted
+// vmcnt wait for exactly this item's loads here (younger prefetches stay in flight), and no later
+// path (switch cases, default) leaves these registers "possibly pending" at a merge point.
+template <int MAXD>
+__device__ __forceinline__ void settle(const ItemBuf<MAXD>& b) {
 #pragma unroll
-  for (int j = 0; j < MAXD; ++j) b.tg[j] = (uint32_t)a.tgt[b.st + min(j, b.d - 1) + z];
+  for (int j = 0; j < MAXD; ++j) asm volatile("" ::"v"(b.row[j]));
+  asm volatile("" ::"v"(b.tgv), "v"(b.chw));
 }
 
 __device__ __forceinline__ uint32_t pack4(const uint32_t (&t)[4]) {
@@ -96,7 +110,9 @@ __device__ __forceinline__ uint32_t pack4(const uint32_t (&t)[4]) {
 template <int D, int MAXD>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
-  uint32_t outw[D];
+  uint32_t outw[D], trow[D];
+#pragma unroll
+  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   const uint32_t fbase = (uint32_t)fslot * kTbl;
   if (do_par) {
     uint32_t par = 0;
@@ -156,7 +172,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
   }
 #pragma unroll
   for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)b.tg[w] * a.ldb + b.cw0) = outw[w];
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.cw0) = outw[w];
 }
 
 // ---------------------------------------------------------------- variable node
@@ -167,7 +183,9 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
 template <int D, int MAXD>
 __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot) {
-  uint32_t outw[D];
+  uint32_t outw[D], trow[D];
+#pragma unroll
+  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   if constexpr (D == 1) {
     outw[0] = b.chw;
   } else {
@@ -205,7 +223,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* l
   }
 #pragma unroll
   for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)b.tg[w] * a.ldb + b.cw0) = outw[w];
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.cw0) = outw[w];
 }
 
 // ------------------------------------------------------------- decision output
@@ -267,11 +285,13 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   const int lane = threadIdx.x & 63;
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
   const int wpb = blockDim.x >> 6;
-  const int gw = blockIdx.x * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
+  // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
   const int nitems = a.n_nodes * a.nchunks;
   const bool do_par = !VN && a.unsat != nullptr;
   bool unsat = false;
   auto compute = [&](const ItemBuf<MAXD>& cur) {
+    settle(cur);
     if constexpr (VN) {
       switch (cur.d) {
         case 1: vn_compute<1, MAXD>(a, lds, lane4, cur, 0); break;
@@ -289,19 +309,23 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
       }
     }
   };
-  // ping-pong buffers (no register copies: a copy would wait for the prefetched loads)
+  // ping-pong buffers (no register copies: a copy would wait for the prefetched loads). The
+  // prefetch is unconditional (clamped to the last item) so the control flow stays straight-line
+  // and the compiler's wait for the current item leaves the next item's loads in flight.
   ItemBuf<MAXD> A, Bb;
   int item = gw;
-  if (item < nitems) fetch_item<MAXD, VN, GATHER>(a, item, lane, A);
-  while (item < nitems) {
+  if (item >= nitems) return;
+  fetch_item<MAXD, VN, GATHER>(a, item, lane, A);
+  for (;;) {
     int next = item + nw;
-    if (next < nitems) fetch_item<MAXD, VN, GATHER>(a, next, lane, Bb);
+    fetch_item<MAXD, VN, GATHER>(a, min(next, nitems - 1), lane, Bb);
     compute(A);
+    if (next >= nitems) break;
     item = next;
-    if (item >= nitems) break;
     next = item + nw;
-    if (next < nitems) fetch_item<MAXD, VN, GATHER>(a, next, lane, A);
+    fetch_item<MAXD, VN, GATHER>(a, min(next, nitems - 1), lane, A);
     compute(Bb);
+    if (next >= nitems) break;
     item = next;
   }
   if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
