@@ -273,7 +273,7 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
 int pick_cfg(int which, int maxd, int nt, int num_cus, KCfg* k) {
   k->lds = (size_t)nt * kTbl;
   int best_waves = 0;
-  for (int block : {512, 1024, 256}) {
+  for (int block : {512, 768, 1024, 384, 640, 256}) {
     int bpc = 0;
     if (ib_fast_occupancy(which, maxd, block, k->lds, &bpc) != hipSuccess) continue;
     const int waves = bpc * block / 64;

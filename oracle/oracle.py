@@ -47,6 +47,11 @@ def lib():
                                        i32, i32, ctypes.c_double, _f64p, i32, i32, _f64p,
                                        ctypes.POINTER(i32), i32]
         L.ibo_max_threads.restype = ctypes.c_int
+        for nm in ("ibo_minsum_fold", "ibo_vn_sum"):
+            getattr(L, nm).restype = ctypes.c_double
+            getattr(L, nm).argtypes = [_f64p, i32]
+        L.ibo_boxplus.restype = ctypes.c_double
+        L.ibo_boxplus.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double]
         _lib = L
     return _lib
 
@@ -99,3 +104,17 @@ def float_decode(g, kind: int, imax: int, llr: np.ndarray, early_stop: bool = Fa
 
 def max_threads() -> int:
     return int(lib().ibo_max_threads())
+
+
+def minsum_fold(m) -> float:
+    m = _c(m, np.float64)
+    return float(lib().ibo_minsum_fold(m, m.size))
+
+
+def vn_sum(m) -> float:
+    m = _c(m, np.float64)
+    return float(lib().ibo_vn_sum(m, m.size))
+
+
+def boxplus(a: float, b: float, llr_max: float = 150.0) -> float:
+    return float(lib().ibo_boxplus(a, b, llr_max))

@@ -1,0 +1,149 @@
+"""CPU: host-side components — loaders, generators, tables, channel model, the C ABI's exported
+symbols and host-only index construction, the drop-in classes' set-up, and the fail-loudly rule."""
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from informationbottleneckdecodingldpc_amd import codes, graph, tables
+from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from informationbottleneckdecodingldpc_amd import _build, _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _build.build()
+    return _lib
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "ibldpc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ibl_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    L = lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 19
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(lib.EXPORTS) == syms
+    assert L.ibl_version() == 1
+
+
+def test_library_device_count_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    assert lib.device_count() == 0
+
+
+@pytest.mark.parametrize("name", ["reg", "wlan"])
+def test_capi_map_node_connections_equals_reference(lib, golden, reg_H, wlan_H, name):
+    """Host-only C ABI entry (no device call) reproduces the reference's index arrays."""
+    H = reg_H if name == "reg" else wlan_H
+    A = codes.canonical_csr(H)
+    out = lib.map_node_connections(A.shape[1], A.shape[0], A.indptr, A.indices)
+    for k, v in out.items():
+        np.testing.assert_array_equal(v, golden[f"{name}_idx_{k}"], err_msg=k)
+
+
+def test_capi_rejects_non_canonical_csr(lib):
+    with pytest.raises(lib.IBLError):
+        lib.map_node_connections(3, 1, np.array([0, 2]), np.array([2, 1]))
+    with pytest.raises(lib.IBLError):
+        lib.map_node_connections(3, 1, np.array([0, 2]), np.array([0, 5]))
+
+
+def test_capi_dvbs2_matches_python_graph(lib, dvb_H):
+    g = graph.build_graph(dvb_H)
+    out = lib.map_node_connections(g.n_v, g.n_c, g.csr_indptr, g.csr_cols)
+    for k, v in out.items():
+        np.testing.assert_array_equal(v, getattr(g, k), err_msg=k)
+
+
+def test_loaders_round_trip(tmp_path, reg_H):
+    A = codes.canonical_csr(reg_H)
+    np.save(tmp_path / "h.npy", A.toarray())
+    codes.save_sparse_csr(str(tmp_path / "h.npz"), A)
+    # alist with weight lines
+    M, N = A.shape
+    csc = A.tocsc()
+    vdeg, cdeg = np.diff(csc.indptr), np.diff(A.indptr)
+    lines = [f"{N} {M}", f"{vdeg.max()} {cdeg.max()}", " ".join(map(str, vdeg)), " ".join(map(str, cdeg))]
+    for j in range(N):
+        r = csc.indices[csc.indptr[j]:csc.indptr[j + 1]] + 1
+        lines.append(" ".join(map(str, np.pad(r, (0, vdeg.max() - r.size)))))
+    (tmp_path / "h.alist").write_text("\n".join(lines) + "\n")
+    for f in ("h.npy", "h.npz", "h.alist"):
+        B = codes.load_check_mat(str(tmp_path / f))
+        assert (B != A).nnz == 0, f
+
+
+def test_regular_code_is_simple_and_regular():
+    H = codes.regular_code(8000, 3, 6, seed=0)
+    g = graph.build_graph(H)
+    assert (g.n_c, g.n_v, g.n_e) == (4000, 8000, 24000)
+    assert set(g.cn_deg) == {6} and set(g.vn_deg) == {3}
+    assert g.R_c == 0.5 and g.data_len == 4000
+
+
+def test_wlan_z81_structure():
+    g = graph.build_graph(codes.wlan_80211n(81))
+    assert (g.n_c, g.n_v) == (972, 1944)
+    assert set(g.cn_deg) == {7, 8} and set(g.vn_deg) == {2, 3, 4, 11}
+
+
+def test_table_lengths_follow_reference_layout():
+    # Discrete_Density_Evolution.py:92-95 / :120-122 for the DVB-S2 profile (SURVEY §8 LUT lengths)
+    assert tables.cn_lut_len(16, 16, 7, 50) == 256 + 4 * 256 + 49 * 5 * 256
+    assert tables.vn_lut_len(16, 16, 8, 50) == 50 * (256 + 7 * 256)
+    tb = tables.random_tables(16, 16, 7, 8, 50, seed=1)
+    tb.check()
+    assert tb.match_cn.size == 50 * 7 * 16 and tb.match_vn.size == 50 * 8 * 16
+    bad = tables.random_tables(16, 16, 7, 8, 5)
+    bad.cn[3] = 16
+    with pytest.raises(ValueError):
+        bad.check()
+
+
+def test_channel_quantizer_contract():
+    q = UniformQuantizer(sigma2_from_ebn0(1.0, 0.5), 16)
+    L = q.output_LLRs
+    assert np.all(np.diff(L) > 0)                  # clusters ordered by LLR
+    np.testing.assert_allclose(L, -L[::-1], atol=1e-9)   # symmetric
+    assert np.all(L[:8] < 0) and np.all(L[8:] > 0)  # cluster < T/2 <=> bit 1
+    t = q.sample_all_zero(1000, 64, np.random.default_rng(0))
+    assert t.min() >= 0 and t.max() <= 15
+    emp = np.bincount(t.ravel(), minlength=16) / t.size
+    np.testing.assert_allclose(emp, q.p_t_given_x0, atol=5e-3)
+    assert sigma2_from_ebn0(0.0, 0.5) == pytest.approx(1.0)
+
+
+def test_dropin_classes_setup_without_gpu(wlan_H, dvb_H):
+    """Constructors are host-only and expose the reference's attributes; decoding without a
+    GPU fails loudly (no CPU fallback)."""
+    import torch
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+        Discrete_LDPC_Decoder_class_irregular
+    g = graph.build_graph(dvb_H)
+    tb = tables.random_tables(16, 16, 7, 8, 10)
+    d = Discrete_LDPC_Decoder_class_irregular(dvb_H, 10, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, 2)
+    assert d.data_len == 32399 and d.R_c == 0.4999999999999999
+    assert d.d_c_max == 7 and d.d_v_max == 8 and d.N_v == 64800
+    np.testing.assert_array_equal(d.target_memory_cells_varnodes, g.tgt_vn)
+    bp = BeliefPropagationDecoderClassIrregular(wlan_H, 10, 16, 4)
+    assert bp.data_len == 648
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        d.decode_OpenCL(np.zeros((64800, 2), dtype=np.int32))
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        bp.decode_OpenCL_belief_propagation(np.zeros((1296, 4)))

@@ -1,0 +1,106 @@
+"""CPU: the oracle and the host-side set-up against the REFERENCE's own outputs.
+
+Golden data (tests/golden/reference_host.npz, wlan_H.npz) was produced by
+tests/golden/make_golden.py, which runs the reference's decoder constructors, its
+decode_on_host and its WLAN generator (imported unchanged, GPU-only imports stubbed).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from informationbottleneckdecodingldpc_amd import codes, graph, tables
+from oracle import oracle
+
+IDX = ["cn_start", "vn_start", "cn_deg", "vn_deg", "tgt_cn", "tgt_vn"]
+
+
+def test_alist_known_answer(golden):
+    # discrete_LDPC_decoder.py:64-67 docstring example, re-run through the reference
+    lines = [[3, 2], [2, 2], [1, 1, 2], [2, 2], [1], [2], [1, 2], [1, 2, 3, 4]]
+    np.testing.assert_array_equal(codes.alist_to_numpy(lines), golden["alist_kat"])
+    np.testing.assert_array_equal(codes.alist_to_numpy(lines), [[1, 0, 1], [0, 1, 1]])
+
+
+def test_wlan_matches_reference_generator(wlan_H):
+    A = codes.wlan_80211n(54)
+    assert (A != wlan_H).nnz == 0
+    g = graph.build_graph(A)
+    assert (g.n_c, g.n_v, g.n_e) == (648, 1296, 4644)
+    assert dict(zip(*np.unique(g.cn_deg, return_counts=True))) == {7: 540, 8: 108}
+    assert dict(zip(*np.unique(g.vn_deg, return_counts=True))) == {2: 594, 3: 486, 4: 54, 11: 162}
+
+
+@pytest.mark.parametrize("name", ["reg", "wlan"])
+def test_index_arrays_equal_reference_map_node_connections(golden, reg_H, wlan_H, name):
+    g = graph.build_graph(reg_H if name == "reg" else wlan_H)
+    for k in IDX:
+        np.testing.assert_array_equal(getattr(g, k), golden[f"{name}_idx_{k}"], err_msg=k)
+    if name == "wlan":
+        assert g.R_c == golden["wlan_R_c"] and g.data_len == golden["wlan_data_len"]
+
+
+def test_dvbs2_structured_profile_and_reference_constructor(golden, dvb_H):
+    g = graph.build_graph(dvb_H)
+    assert (g.n_c, g.n_v, g.n_e) == (32400, 64800, 226799)
+    assert dict(zip(*np.unique(g.cn_deg, return_counts=True))) == {6: 1, 7: 32399}
+    assert dict(zip(*np.unique(g.vn_deg, return_counts=True))) == {1: 1, 2: 32399, 3: 19440, 8: 12960}
+    assert g.vn_deg[64799] == 1 and g.cn_deg[0] == 6
+    # index arrays and rate bit-identical to the reference constructor run on the same H
+    for k in IDX:
+        dig = hashlib.sha256(np.ascontiguousarray(getattr(g, k).astype(np.int32))).digest()
+        assert dig == golden[f"dvb_idx_sha256_{k}"].tobytes(), k
+    assert g.R_c == golden["dvb_R_c"] == 0.4999999999999999
+    assert g.data_len == golden["dvb_data_len"] == 32399
+
+
+@pytest.mark.parametrize("name,CM,VM", [("reg", 6, 3), ("wlan", 8, 11)])
+@pytest.mark.parametrize("imax", [1, 2, 10])
+def test_oracle_equals_reference_decode_on_host(golden, reg_H, wlan_H, name, CM, VM, imax):
+    """Oracle (match off, no early stop, one codeword per column) == reference decode_on_host."""
+    g = graph.build_graph(reg_H if name == "reg" else wlan_H)
+    z = golden
+    tb = tables.IBTables(16, 16, CM, VM, imax, z[f"{name}_imax{imax}_cn"], z[f"{name}_imax{imax}_vn"],
+                         tables.identity_matching(16, CM, imax), tables.identity_matching(16, VM, imax))
+    out = oracle.ib_decode(g, tb, z[f"{name}_imax{imax}_ch"], match=False)
+    np.testing.assert_array_equal(out, z[f"{name}_imax{imax}_out"])
+
+
+def test_oracle_columns_are_independent(wlan_H):
+    """Without early stop the batch is just independent codewords (column-wise decoding)."""
+    g = graph.build_graph(wlan_H)
+    tb = tables.random_tables(16, 16, 8, 11, 5, seed=4)
+    ch = np.random.default_rng(0).integers(0, 16, (g.n_v, 5))
+    full = oracle.ib_decode(g, tb, ch, match=True)
+    for b in range(5):
+        np.testing.assert_array_equal(oracle.ib_decode(g, tb, ch[:, b], match=True)[:, 0], full[:, b])
+
+
+def test_oracle_minsum_node_ops_equal_reference(golden):
+    """min-sum CN fold and VN sum == the reference's host operations
+    (min_sum_decoder_irreg.py:298-320), including zero inputs."""
+    a = np.array([oracle.minsum_fold(r) for r in golden["ms_cn_in"]])
+    np.testing.assert_array_equal(a, golden["ms_cn_out"])
+    b = np.array([oracle.vn_sum(r) for r in golden["ms_vn_in"]])
+    np.testing.assert_array_equal(b, golden["ms_vn_out"])
+
+
+def test_oracle_boxplus_formula():
+    """kernels_min_and_BP.cl:5-9: log((1+e^(a+b))/(e^a+e^b)), clamped to +-150."""
+    for a, b in [(1.0, 2.0), (-3.0, 0.5), (20.0, -20.0), (0.0, 5.0)]:
+        ref = np.log((1 + np.exp(a + b)) / (np.exp(a) + np.exp(b)))
+        assert oracle.boxplus(a, b) == pytest.approx(ref, abs=1e-12)
+    assert oracle.boxplus(140.0, 140.0) <= 150.0
+
+
+def test_llr_tables_decode_on_oracle(wlan_H):
+    """The LLR-quantised table generator yields a working decoder (all-zero codeword, 5 dB)."""
+    from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+    g = graph.build_graph(wlan_H)
+    q = UniformQuantizer(sigma2_from_ebn0(5.0, g.R_c), 16)
+    tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 20)
+    tb.check()
+    ch = q.sample_all_zero(g.n_v, 8, np.random.default_rng(5))
+    out = oracle.ib_decode(g, tb, ch, match=True, early_stop=True)
+    assert (out[:g.data_len] < 8).sum() == 0
