@@ -10,6 +10,7 @@
 // pass uses.  The host only enqueues.
 #include <algorithm>
 #include <functional>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,9 +29,19 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+// IBL_DEBUG_SYNC=1: synchronise after every launch so an asynchronous fault is reported at the
+// launch that caused it (debugging only; breaks the no-host-sync property of decode).
+static bool debug_sync() {
+  static const bool on = [] {
+    const char* v = getenv("IBL_DEBUG_SYNC");
+    return v && *v && *v != '0';
+  }();
+  return on;
+}
 #define HIPCHK(expr)                                                                        \
   do {                                                                                      \
     hipError_t _e = (expr);                                                                 \
+    if (_e == hipSuccess && debug_sync()) _e = hipDeviceSynchronize();                      \
     if (_e != hipSuccess)                                                                   \
       return fail(IBL_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));            \
   } while (0)
@@ -323,7 +334,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
   h->g = g;
   h->Tc = Tc; h->T = T; h->imax = imax; h->CM = CM; h->VM = VM; h->match = match ? 1 : 0;
   h->max_batch = max_batch;
-  h->ldb = (max_batch + kChunk - 1) / kChunk * kChunk;
+  h->ldb = (max_batch + kChunkIB - 1) / kChunkIB * kChunkIB;   // codewords; fast path rows = ldb/2 bytes
   auto bail = [&](int rc) { ibl_ib_destroy(h); return rc; };
   int rc;
   const size_t inbox = (size_t)g->n_e * h->ldb;
@@ -456,16 +467,17 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
   const int I = h->imax;
   const bool early = early_stop != 0 && I > 1;
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
-  HIPCHK(launch_ib_stage(d_ch, ch_dtype, g->n_v, B, h->ch8, h->ldb, s));
-  const int nchunks = (B + kChunk - 1) / kChunk;
   if (h->fast) {
+    const int nchunks = (B + kChunkIB - 1) / kChunkIB;
+    const int ldbb = h->ldb / 2;
+    HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     IbFastArgs cn{}, vn{};
     cn.ch8 = vn.ch8 = h->ch8;
     cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin;
     vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
     cn.nchunks = vn.nchunks = nchunks;
-    cn.ldb = vn.ldb = h->ldb;
+    cn.ldb = vn.ldb = ldbb;
     cn.B = vn.B = B;
     cn.half = vn.half = h->T / 2;
     cn.match = vn.match = h->match;
@@ -490,11 +502,12 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     IbDecArgs dc{};
     dc.vin = h->vin; dc.ch8 = h->ch8; dc.start = g->vn_start; dc.deg = g->vn_deg; dc.img = h->dec_img;
     dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.nt = h->dec_nt; dc.n_nodes = g->n_v;
-    dc.nchunks = nchunks; dc.ldb = h->ldb; dc.B = B;
+    dc.nchunks = nchunks; dc.ldb = ldbb; dc.B = B;
     const size_t esz = out_dtype == kU8 ? 1 : 4;
     dc.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
     HIPCHK(launch_ib_dec_fast(dc, h->kdec.grid, h->kdec.block, h->kdec.lds, s));
   } else {
+    HIPCHK(launch_ib_stage(d_ch, ch_dtype, g->n_v, B, h->ch8, h->ldb, s));
     IbGenArgs cn{}, vn{};
     cn.ch8 = vn.ch8 = h->ch8;
     cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin; cn.lut = h->cn_lut;

@@ -14,7 +14,8 @@
 namespace ibl {
 
 constexpr int kWave = 64;
-constexpr int kChunk = 256;       // codewords per wave item (u8: 4 per lane, fp32: 4, fp64: 2x2)
+constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, fp64: 2x2)
+constexpr int kChunkIB = 512;     // IB fast path: 4-bit messages, 8 codewords per lane
 constexpr int kTbl = 8192;        // one IB lookup table replicated over the 32 LDS banks
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
 constexpr int kMaxD = 16;         // largest node degree with an unrolled fast-path body
@@ -27,7 +28,7 @@ enum Dtype : int32_t { kU8 = 1, kI32 = 2, kF32 = 3, kF64 = 4 };
 struct IbFastArgs {
   const uint8_t* in;        // own-order inbox (nullptr for CN pass 0: inputs gathered from ch8)
   uint8_t* out;             // other-order inbox
-  const uint8_t* ch8;       // staged channel cluster ids [N][ldb]
+  const uint8_t* ch8;       // staged channel cluster ids: 4-bit nibbles [N][ldb bytes]
   const int32_t* start;     // node -> first own-order edge
   const int32_t* deg;       // node degree
   const int32_t* tgt;       // own-order edge -> other-order row
@@ -37,7 +38,7 @@ struct IbFastArgs {
   int32_t* unsat;           // kShards flag words to set when a check is unsatisfied (nullptr: no syndrome)
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
   int32_t nt;               // tables staged in LDS
-  int32_t n_nodes, nchunks, ldb, B, half, match;
+  int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
 };
 
 struct IbDecArgs {
@@ -108,6 +109,7 @@ struct FlDecArgs {
 
 // launchers (defined in the .hip translation units, called by capi.hip)
 hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb, hipStream_t s);
+hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s);
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);

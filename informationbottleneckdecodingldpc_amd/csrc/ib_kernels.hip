@@ -52,16 +52,28 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
   for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
 }
 
+// Fast-path message format: T <= 16, so every message is a 4-bit nibble; an edge row stores
+// codeword c in nibble (c & 1) of byte c/2. A lane owns 8 consecutive codewords = one dword of
+// each row, a wave item = one node x kChunkN = 512 codewords (256-B row segments per wave).
+constexpr int kChunkN = 512;
+
+__device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
+
+__device__ __forceinline__ uint32_t valid_mask8(int remaining) {
+  return remaining >= 8 ? 0xFFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
+}
+
 // A wave item's inputs, fetched one item ahead of its computation (register double buffer):
 // the row loads of item k+1 are issued before item k is computed, so HBM latency overlaps the
 // lookups and the waits never cover the previous item's stores.
 template <int MAXD>
 struct ItemBuf {
-  uint32_t row[MAXD];   // 4 packed u8 messages (codewords cw0..cw0+3) of each input row
+  uint32_t row[MAXD];   // 8 packed 4-bit messages (codewords cwb..cwb+7) of each input row
   uint32_t tgv;         // lane j < d holds the destination row tgt[st + j] of output edge j
-  uint32_t chw;         // channel values (VN) of the same 4 codewords
+  uint32_t chw;         // channel values (VN) of the same 8 codewords
   int d, st, node;
-  uint32_t cw0;
+  uint32_t off;         // byte offset of this lane's dword in a row
+  int cwb;              // first codeword of this lane
 };
 
 template <int MAXD, bool VN, bool GATHER>
@@ -71,16 +83,17 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.node = node;
   b.d = sload(a.deg, node);
   b.st = sload(a.start, node);
-  b.cw0 = (uint32_t)(chunk * kChunk + lane * 4);
+  b.off = (uint32_t)(chunk * (kChunkN / 2) + lane * 4);
+  b.cwb = chunk * kChunkN + lane * 8;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    b.row[j] = *reinterpret_cast<const uint32_t*>(row + b.cw0);
+    b.row[j] = *reinterpret_cast<const uint32_t*>(row + b.off);
   }
-  if (VN) b.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + b.cw0);
+  if (VN) b.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + b.off);
   else b.chw = 0;
   // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
   // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
@@ -97,8 +110,9 @@ __device__ __forceinline__ void settle(const ItemBuf<MAXD>& b) {
   asm volatile("" ::"v"(b.tgv), "v"(b.chw));
 }
 
-__device__ __forceinline__ uint32_t pack4(const uint32_t (&t)[4]) {
-  return t[0] | (t[1] << 8) | (t[2] << 16) | (t[3] << 24);
+// nibbles 4g..4g+3 of an output word
+__device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
+  return (t[0] | (t[1] << 4) | (t[2] << 8) | (t[3] << 12)) << (16 * g);
 }
 
 // ------------------------------------------------------------------ check node
@@ -106,73 +120,82 @@ __device__ __forceinline__ uint32_t pack4(const uint32_t (&t)[4]) {
 // other inputs with table l at fold step l (kernels_template_irreg.cl:226-231):
 //   out[0]   = fold(in_1, in_2, ...),   out[w] = fold(P_w, in_{w+1}, ...),  P_w = fold(in_0..in_{w-1})
 // Step l uses LDS slot l, except the last step (l = D-3) which uses fslot (matching composed).
-// The 4 codewords of a lane are advanced together so each fold step issues 4 independent reads.
+// The lane's 8 codewords run as two groups of 4 advanced together (4 independent reads per step).
 template <int D, int MAXD>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
   uint32_t outw[D], trow[D];
 #pragma unroll
-  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
+  for (int w = 0; w < D; ++w) {
+    trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
+    outw[w] = 0;
+  }
   const uint32_t fbase = (uint32_t)fslot * kTbl;
   if (do_par) {
     uint32_t par = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int k = 0; k < 8; ++k) {
       uint32_t p = 0;
 #pragma unroll
-      for (int j = 0; j < D; ++j) p ^= (__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8) < (uint32_t)a.half) ? 1u : 0u;
-      par |= p << s;
+      for (int j = 0; j < D; ++j) p ^= (nib(b.row[j], k) < (uint32_t)a.half) ? 1u : 0u;
+      par |= p << k;
     }
-    if (par & valid_mask4(a.B - (int)b.cw0)) unsat = true;
+    if (par & valid_mask8(a.B - b.cwb)) unsat = true;
   }
   if constexpr (D == 2) {
     if (a.match) {
-      uint32_t t0[4], t1[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        t0[s] = lds[(__builtin_amdgcn_ubfe(b.row[1], 8 * s, 8) << 9) + lane4 + fbase];
-        t1[s] = lds[(__builtin_amdgcn_ubfe(b.row[0], 8 * s, 8) << 9) + lane4 + fbase];
+      for (int g = 0; g < 2; ++g) {
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0[s] = lds[(nib(b.row[1], 4 * g + s) << 9) + lane4 + fbase];
+          t1[s] = lds[(nib(b.row[0], 4 * g + s) << 9) + lane4 + fbase];
+        }
+        outw[0] |= pack4n(t0, g);
+        outw[1] |= pack4n(t1, g);
       }
-      outw[0] = pack4(t0);
-      outw[1] = pack4(t1);
     } else {
       outw[0] = b.row[1];
       outw[1] = b.row[0];
     }
   } else {
-    uint32_t q[D][4];
-#pragma unroll
-    for (int j = 1; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) q[j][s] = qidx(__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8), lane4);
     auto sb = [&](int l) -> uint32_t { return (l == D - 3) ? fbase : (uint32_t)(l * kTbl); };
-    uint32_t t[4], P[4];
+#pragma unroll 1
+    for (int g = 0; g < 2; ++g) {
+      uint32_t q[D][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = __builtin_amdgcn_ubfe(b.row[1], 8 * s, 8);
+      for (int j = 1; j < D; ++j)
 #pragma unroll
-    for (int j = 2; j < D; ++j)
+        for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(b.row[j], 4 * g + s), lane4);
+      uint32_t t[4], P[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
-    outw[0] = pack4(t);
+      for (int s = 0; s < 4; ++s) t[s] = nib(b.row[1], 4 * g + s);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) P[s] = __builtin_amdgcn_ubfe(b.row[0], 8 * s, 8);
-#pragma unroll
-    for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = P[s];
-#pragma unroll
-      for (int j = w + 1; j < D; ++j)
+      for (int j = 2; j < D; ++j)
 #pragma unroll
         for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
-      outw[w] = pack4(t);
+      outw[0] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
+      for (int s = 0; s < 4; ++s) P[s] = nib(b.row[0], 4 * g + s);
+#pragma unroll
+      for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = P[s];
+#pragma unroll
+        for (int j = w + 1; j < D; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+        outw[w] |= pack4n(t, g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
+      }
+      outw[D - 1] |= pack4n(P, g);
     }
-    outw[D - 1] = pack4(P);
   }
 #pragma unroll
   for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.cw0) = outw[w];
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off) = outw[w];
 }
 
 // ---------------------------------------------------------------- variable node
@@ -185,50 +208,56 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* l
                                            const ItemBuf<MAXD>& b, int fslot) {
   uint32_t outw[D], trow[D];
 #pragma unroll
-  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
+  for (int w = 0; w < D; ++w) {
+    trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
+    outw[w] = 0;
+  }
   if constexpr (D == 1) {
     outw[0] = b.chw;
   } else {
     const uint32_t fbase = (uint32_t)fslot * kTbl;
     auto sb = [&](int l) -> uint32_t { return (l == D - 2) ? fbase : (uint32_t)(l * kTbl); };
-    uint32_t q[D][4], c[4], t[4], Q[4];
+#pragma unroll 1
+    for (int g = 0; g < 2; ++g) {
+      uint32_t q[D][4], c[4], t[4], Q[4];
 #pragma unroll
-    for (int j = 0; j < D; ++j)
+      for (int j = 0; j < D; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) q[j][s] = qidx(__builtin_amdgcn_ubfe(b.row[j], 8 * s, 8), lane4);
+        for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(b.row[j], 4 * g + s), lane4);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) c[s] = __builtin_amdgcn_ubfe(b.chw, 8 * s, 8) << 9;
+      for (int s = 0; s < 4; ++s) c[s] = nib(b.chw, 4 * g + s) << 9;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
+      for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
 #pragma unroll
-    for (int j = 2; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
-    outw[0] = pack4(t);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
-#pragma unroll
-    for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = Q[s];
-#pragma unroll
-      for (int j = w + 1; j < D; ++j)
+      for (int j = 2; j < D; ++j)
 #pragma unroll
         for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
-      outw[w] = pack4(t);
+      outw[0] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+      for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
+#pragma unroll
+      for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = Q[s];
+#pragma unroll
+        for (int j = w + 1; j < D; ++j)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+        outw[w] |= pack4n(t, g);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+      }
+      outw[D - 1] |= pack4n(Q, g);
     }
-    outw[D - 1] = pack4(Q);
   }
 #pragma unroll
   for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.cw0) = outw[w];
+    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off) = outw[w];
 }
 
 // ------------------------------------------------------------- decision output
 // calc_varnode_output (kernels_template_irreg.cl:279-300): fold of channel and ALL inputs with
-// the raw tables V_0..V_{D-1} of pass L, no matching.
+// the raw tables V_0..V_{D-1} of pass L, no matching. Writes 4 consecutive codewords.
 __device__ __forceinline__ void store4(void* out, int dtype, size_t row_off, int cw0, int B, bool aligned,
                                        uint32_t packed) {
   if (dtype == kU8) {
@@ -255,22 +284,24 @@ __device__ __forceinline__ void store4(void* out, int dtype, size_t row_off, int
 
 template <int D>
 __device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds, uint32_t lane4, int node,
-                                         int st, uint32_t cw0) {
+                                         int st, uint32_t off, int cwb) {
   uint32_t inw[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) inw[j] = *reinterpret_cast<const uint32_t*>(a.vin + (size_t)(st + j) * a.ldb + cw0);
-  const uint32_t cw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + cw0);
-  uint32_t packed = 0;
+  for (int j = 0; j < D; ++j) inw[j] = *reinterpret_cast<const uint32_t*>(a.vin + (size_t)(st + j) * a.ldb + off);
+  const uint32_t cw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + off);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const uint32_t c = __builtin_amdgcn_ubfe(cw, 8 * s, 8);
-    uint32_t Q = lds[(c << 9) + qidx(__builtin_amdgcn_ubfe(inw[0], 8 * s, 8), lane4)];
+  for (int g = 0; g < 2; ++g) {
+    uint32_t packed = 0;
 #pragma unroll
-    for (int k = 1; k < D; ++k)
-      Q = lds[(Q << 9) + qidx(__builtin_amdgcn_ubfe(inw[k], 8 * s, 8), lane4) + k * kTbl];
-    packed |= Q << (8 * s);
+    for (int s = 0; s < 4; ++s) {
+      const int k = 4 * g + s;
+      uint32_t Q = lds[(nib(cw, k) << 9) + qidx(nib(inw[0], k), lane4)];
+#pragma unroll
+      for (int l = 1; l < D; ++l) Q = lds[(Q << 9) + qidx(nib(inw[l], k), lane4) + l * kTbl];
+      packed |= Q << (8 * s);
+    }
+    store4(a.out, a.out_dtype, (size_t)node * a.B, cwb + 4 * g, a.B, a.aligned != 0, packed);
   }
-  store4(a.out, a.out_dtype, (size_t)node * a.B, (int)cw0, a.B, a.aligned != 0, packed);
 }
 
 // ---------------------------------------------------------------------- kernels
@@ -331,8 +362,10 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
 }
 
+// MAXD=16 bodies need more than the 128 VGPRs a 1024-thread block allows: cap those at 512
+// threads (256 VGPRs, no scratch spill); the MAXD=8 bodies fit 1024-thread blocks.
 template <int MAXD, bool GATHER>
-__global__ __launch_bounds__(1024) void ib_cn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? 1024 : 512) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   stage_tables(lds, a.img, a.nt);
@@ -341,7 +374,7 @@ __global__ __launch_bounds__(1024) void ib_cn_fast(IbFastArgs a) {
 }
 
 template <int MAXD>
-__global__ __launch_bounds__(1024) void ib_vn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? 1024 : 512) void ib_vn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
   stage_tables(lds, a.img, a.nt);
@@ -363,11 +396,12 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
     const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
     const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
     const int d = a.deg[node], st = a.start[node];
-    const uint32_t cw0 = (uint32_t)(chunk * kChunk + lane * 4);
-    if ((int)cw0 >= a.B) continue;
+    const uint32_t off = (uint32_t)(chunk * (kChunkN / 2) + lane * 4);
+    const int cwb = chunk * kChunkN + lane * 8;
+    if (cwb >= a.B) continue;
     switch (d) {
-      case 1: dec_item<1>(a, lds, lane4, node, st, cw0); break;
-#define X(D) case D: dec_item<D>(a, lds, lane4, node, st, cw0); break;
+      case 1: dec_item<1>(a, lds, lane4, node, st, off, cwb); break;
+#define X(D) case D: dec_item<D>(a, lds, lane4, node, st, off, cwb); break;
       IBL_DEG_CASES(X)
 #undef X
       default: break;
@@ -398,6 +432,32 @@ __global__ void ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, 
       packed |= v << (8 * s);
     }
     *reinterpret_cast<uint32_t*>(ch8 + (size_t)row * ldb + cw0) = packed;
+  }
+}
+
+// ------------------------------------------- channel staging for the fast path (-> 4-bit nibbles)
+__global__ void ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes) {
+  const int words = ldb_bytes >> 2;
+  const size_t total = (size_t)n * words;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / words);
+    const int cw0 = (int)(i - (size_t)row * words) * 8;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int cw = cw0 + s;
+      uint32_t v = 0;
+      if (cw < B) {
+        if (dtype == kU8) {
+          v = reinterpret_cast<const uint8_t*>(ch)[(size_t)row * B + cw];
+        } else {
+          const int32_t x = reinterpret_cast<const int32_t*>(ch)[(size_t)row * B + cw];
+          v = (uint32_t)min(max(x, 0), 255);
+        }
+      }
+      packed |= min(v, 15u) << (4 * s);
+    }
+    *reinterpret_cast<uint32_t*>(ch4 + (size_t)row * ldb_bytes + cw0 / 2) = packed;
   }
 }
 
@@ -544,6 +604,12 @@ hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8
   const size_t total = (size_t)n * (ldb / 4);
   const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(ib_stage, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, ch8, ldb);
+  return hipGetLastError();
+}
+hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s) {
+  const size_t total = (size_t)n * (ldb_bytes / 4);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(ib_stage4, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, ch4, ldb_bytes);
   return hipGetLastError();
 }
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
