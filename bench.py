@@ -139,24 +139,40 @@ def main():
     value = world * B * a.steps / elapsed
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
+    # SURVEY §8(d) per-unit figures (u8 messages for IB, fp32 for float) x codewords per launch
     cn_bytes = 2 * g.n_e * w * B
     vn_bytes = (2 * g.n_e * w + n_v * w) * B
+    # bytes actually stored by this build: the IB fast path keeps 4-bit messages/channel values
+    ws = 0.5 if (a.kind == "ib" and getattr(dec, "fast_path", False)) else w
+    fmt = {0.5: "u4", 1: "u8", 4: "f32"}[ws]
     if vn_ms >= cn_ms:
-        kname, kavg, kbytes = ("ib_vn_fast" if a.kind == "ib" else "fl_vn"), vn_avg, vn_bytes
+        kname, kavg, kbytes, kstored = ("ib_vn_fast" if a.kind == "ib" else "fl_vn"), vn_avg, vn_bytes, int(vn_bytes * ws / w)
     else:
-        kname, kavg, kbytes = ("ib_cn_fast" if a.kind == "ib" else "fl_cn"), cn_avg, cn_bytes
+        kname, kavg, kbytes, kstored = ("ib_cn_fast" if a.kind == "ib" else "fl_cn"), cn_avg, cn_bytes, int(cn_bytes * ws / w)
     achieved = kbytes / (kavg * 1e-3) / 1e9 if kavg > 0 else 0.0
+    achieved_stored = kstored / (kavg * 1e-3) / 1e9 if kavg > 0 else 0.0
     traffic = None
     if os.path.exists(a.pmc):
         try:
             with open(a.pmc) as fh:
                 pm = json.load(fh)
             ent = pm.get(a.kind, {}).get(kname)
-            if ent and int(ent.get("batch", -1)) == B:
+            if ent and int(ent.get("batch", -1)) == B and ent.get("format") == fmt:
                 traffic = ent.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-
+    lds = None
+    if a.kind == "ib" and getattr(dec, "fast_path", False):
+        # table lookups per codeword and pass of the fast path (prefix sharing, matching composed)
+        def cn_lk(d):
+            return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
+        def vn_lk(d):
+            return 0 if d == 1 else (d - 1) + d * (d - 1) // 2
+        lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
+        avg = {"cn": cn_avg, "vn": vn_avg}
+        # per CU and clock at the 2.4 GHz max clock, 256 CUs; LDS ceiling 32 conflict-free ds_read_u8 lanes/clk/CU
+        lds = {k: round(lk[k] / (avg[k] * 1e-3) / (256 * 2.4e9), 2) for k in lk}
+        lds["ceiling"] = 32.0
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.kind == "ib":
         from oracle import oracle
@@ -198,6 +214,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "bytes_per_launch": kbytes, "avg_launch_ms": round(kavg, 4),
+                         "stored_format": fmt, "stored_bytes_per_launch": kstored,
+                         "achieved_stored": round(achieved_stored, 1),
+                         "frac_stored": round(achieved_stored / HBM_PEAK_GBPS, 4),
+                         "lds_lookups_per_clk_per_cu": lds,
                          "launches": {"cn": cn_n, "vn": vn_n},
                          "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}},
             "cpu_baseline": cpu,

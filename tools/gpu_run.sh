@@ -33,6 +33,12 @@ for s in $STEPS; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/bench_pmc_$c.json 2> $O/pmc_$c.err)
         rc=$?; echo "pmc $c rc=$rc" >> $O/summary.txt; crash $rc pmc_$c
       done;;
+    sq)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE -d $O/pmc_SQ -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/bench_pmc_sq.json 2> $O/pmc_sq.err)
+      rc=$?; echo "pmc SQ rc=$rc" >> $O/summary.txt; crash $rc pmc_sq;;
+    sq2)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d $O/pmc_SQ2 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/bench_pmc_sq2.json 2> $O/pmc_sq2.err)
+      rc=$?; echo "pmc SQ2 rc=$rc" >> $O/summary.txt; crash $rc pmc_sq2;;
   esac
 done
 echo done >> $O/summary.txt
