@@ -25,8 +25,10 @@ def _stale(out: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    objdir = os.path.join(PKG, "build")
+def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB, tag: str = "") -> str:
+    """Compile the HIP sources and link `lib`. `defines` (e.g. ["IBL_W=2"]) select kernel variants;
+    variant objects go to build/<tag>/."""
+    objdir = os.path.join(PKG, "build", tag) if tag else os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
     headers = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "ibldpc.h")]
     jobs = []
@@ -34,7 +36,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         s = os.path.join(CSRC, src)
         o = os.path.join(objdir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, "-c", s, "-o", o])
+            jobs.append([HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", s, "-o", o])
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
@@ -44,13 +46,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
                 if verbose:
                     sys.stderr.write(r.stderr)
     objs = [os.path.join(objdir, s.replace(".hip", ".o")) for s in SOURCES]
-    if force or jobs or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+    if force or jobs or _stale(lib, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)
             raise RuntimeError("link failed")
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libibldpc.so")
+# IBLDPC_LIB selects an alternative in-tree build (kernel variants, see tools/variants.py)
+LIB_PATH = os.environ.get("IBLDPC_LIB") or os.path.join(_HERE, "libibldpc.so")
 
 IBL_OK, IBL_EINVAL, IBL_EHIP, IBL_ENOMEM, IBL_EUNSUPPORTED = 0, -1, -2, -3, -4
 IBL_U8, IBL_I32, IBL_F32, IBL_F64 = 1, 2, 3, 4

@@ -502,7 +502,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     IbDecArgs dc{};
     dc.vin = h->vin; dc.ch8 = h->ch8; dc.start = g->vn_start; dc.deg = g->vn_deg; dc.img = h->dec_img;
     dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.nt = h->dec_nt; dc.n_nodes = g->n_v;
-    dc.nchunks = nchunks; dc.ldb = ldbb; dc.B = B;
+    dc.nchunks = (B + kChunkDec - 1) / kChunkDec; dc.ldb = ldbb; dc.B = B;
     const size_t esz = out_dtype == kU8 ? 1 : 4;
     dc.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
     HIPCHK(launch_ib_dec_fast(dc, h->kdec.grid, h->kdec.block, h->kdec.lds, s));

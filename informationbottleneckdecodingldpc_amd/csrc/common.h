@@ -15,7 +15,13 @@ namespace ibl {
 
 constexpr int kWave = 64;
 constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, fp64: 2x2)
-constexpr int kChunkIB = 512;     // IB fast path: 4-bit messages, 8 codewords per lane
+// IB fast path: 4-bit messages; a lane owns IBL_W dwords (8*IBL_W codewords) of each edge row
+#ifndef IBL_W
+#define IBL_W 1
+#endif
+constexpr int kW = IBL_W;
+constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
+constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item
 constexpr int kTbl = 8192;        // one IB lookup table replicated over the 32 LDS banks
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
 constexpr int kMaxD = 16;         // largest node degree with an unrolled fast-path body

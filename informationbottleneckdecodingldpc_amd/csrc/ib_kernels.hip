@@ -53,14 +53,40 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
 }
 
 // Fast-path message format: T <= 16, so every message is a 4-bit nibble; an edge row stores
-// codeword c in nibble (c & 1) of byte c/2. A lane owns 8 consecutive codewords = one dword of
-// each row, a wave item = one node x kChunkN = 512 codewords (256-B row segments per wave).
-constexpr int kChunkN = 512;
-
+// codeword c in nibble (c & 1) of byte c/2. A lane owns 8*kW consecutive codewords = kW dwords of
+// each row, a wave item = one node x kChunkIB codewords (256*kW-B row segments per wave).
 __device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
 
 __device__ __forceinline__ uint32_t valid_mask8(int remaining) {
   return remaining >= 8 ? 0xFFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
+}
+
+template <int W> struct RowVec;
+template <> struct RowVec<1> { typedef uint32_t T; };
+template <> struct RowVec<2> { typedef uint2 T; };
+template <> struct RowVec<4> { typedef uint4 T; };
+
+template <int W>
+__device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&r)[W]) {
+  const auto v = *reinterpret_cast<const typename RowVec<W>::T*>(p);
+  if constexpr (W == 1) {
+    r[0] = v;
+  } else if constexpr (W == 2) {
+    r[0] = v.x; r[1] = v.y;
+  } else {
+    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void store_row(uint8_t* p, const uint32_t (&r)[W]) {
+  if constexpr (W == 1) {
+    *reinterpret_cast<uint32_t*>(p) = r[0];
+  } else if constexpr (W == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(r[0], r[1]);
+  } else {
+    *reinterpret_cast<uint4*>(p) = make_uint4(r[0], r[1], r[2], r[3]);
+  }
 }
 
 // A wave item's inputs, fetched one item ahead of its computation (register double buffer):
@@ -68,12 +94,12 @@ __device__ __forceinline__ uint32_t valid_mask8(int remaining) {
 // lookups and the waits never cover the previous item's stores.
 template <int MAXD>
 struct ItemBuf {
-  uint32_t row[MAXD];   // 8 packed 4-bit messages (codewords cwb..cwb+7) of each input row
-  uint32_t tgv;         // lane j < d holds the destination row tgt[st + j] of output edge j
-  uint32_t chw;         // channel values (VN) of the same 8 codewords
+  uint32_t row[MAXD][kW];  // 8*kW packed 4-bit messages (codewords cwb..) of each input row
+  uint32_t tgv;            // lane j < d holds the destination row tgt[st + j] of output edge j
+  uint32_t chw[kW];        // channel values (VN) of the same codewords
   int d, st, node;
-  uint32_t off;         // byte offset of this lane's dword in a row
-  int cwb;              // first codeword of this lane
+  uint32_t off;            // byte offset of this lane's words in a row
+  int cwb;                 // first codeword of this lane
 };
 
 template <int MAXD, bool VN, bool GATHER>
@@ -83,18 +109,22 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.node = node;
   b.d = sload(a.deg, node);
   b.st = sload(a.start, node);
-  b.off = (uint32_t)(chunk * (kChunkN / 2) + lane * 4);
-  b.cwb = chunk * kChunkN + lane * 8;
+  b.off = (uint32_t)(chunk * (kChunkIB / 2) + lane * 4 * kW);
+  b.cwb = chunk * kChunkIB + lane * 8 * kW;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    b.row[j] = *reinterpret_cast<const uint32_t*>(row + b.off);
+    load_row<kW>(row + b.off, b.row[j]);
   }
-  if (VN) b.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + b.off);
-  else b.chw = 0;
+  if (VN) {
+    load_row<kW>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kW; ++i) b.chw[i] = 0;
+  }
   // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
   // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
   b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
@@ -106,8 +136,12 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
 template <int MAXD>
 __device__ __forceinline__ void settle(const ItemBuf<MAXD>& b) {
 #pragma unroll
-  for (int j = 0; j < MAXD; ++j) asm volatile("" ::"v"(b.row[j]));
-  asm volatile("" ::"v"(b.tgv), "v"(b.chw));
+  for (int j = 0; j < MAXD; ++j)
+#pragma unroll
+    for (int i = 0; i < kW; ++i) asm volatile("" ::"v"(b.row[j][i]));
+#pragma unroll
+  for (int i = 0; i < kW; ++i) asm volatile("" ::"v"(b.chw[i]));
+  asm volatile("" ::"v"(b.tgv));
 }
 
 // nibbles 4g..4g+3 of an output word
@@ -115,87 +149,120 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
   return (t[0] | (t[1] << 4) | (t[2] << 8) | (t[3] << 12)) << (16 * g);
 }
 
+// Group loop (two groups of 4 codewords per dword): rolled keeps VGPRs low (more waves), unrolled
+// gives 8 independent chains per step.
+#ifndef IBL_CN_UNROLL
+#define IBL_CN_UNROLL 0
+#endif
+#ifndef IBL_VN_UNROLL
+#define IBL_VN_UNROLL 0
+#endif
+
 // ------------------------------------------------------------------ check node
 // Inputs in_0..in_{D-1} (CN order = ascending column). Output w is the left fold over the
 // other inputs with table l at fold step l (kernels_template_irreg.cl:226-231):
 //   out[0]   = fold(in_1, in_2, ...),   out[w] = fold(P_w, in_{w+1}, ...),  P_w = fold(in_0..in_{w-1})
 // Step l uses LDS slot l, except the last step (l = D-3) which uses fslot (matching composed).
-// The lane's 8 codewords run as two groups of 4 advanced together (4 independent reads per step).
+// One dword of each row = 8 codewords, run as two groups of 4 (4 independent reads per step).
+template <int D>
+__device__ __forceinline__ void cn_word(const uint8_t* lds, uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
+                                        uint32_t (&outw)[D]) {
+  auto sb = [&](int l) -> uint32_t { return (l == D - 3) ? fbase : (uint32_t)(l * kTbl); };
+#if IBL_CN_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+  for (int g = 0; g < 2; ++g) {
+    uint32_t q[D][4];
+#pragma unroll
+    for (int j = 1; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
+    uint32_t t[4], P[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) t[s] = nib(in[1], 4 * g + s);
+#pragma unroll
+    for (int j = 2; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+    outw[0] |= pack4n(t, g);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) P[s] = nib(in[0], 4 * g + s);
+#pragma unroll
+    for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = P[s];
+#pragma unroll
+      for (int j = w + 1; j < D; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+      outw[w] |= pack4n(t, g);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
+    }
+    outw[D - 1] |= pack4n(P, g);
+  }
+}
+
 template <int D, int MAXD>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
-  uint32_t outw[D], trow[D];
+  uint32_t outw[D][kW], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) {
     trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
-    outw[w] = 0;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) outw[w][i] = 0;
   }
   const uint32_t fbase = (uint32_t)fslot * kTbl;
   if (do_par) {
-    uint32_t par = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      uint32_t p = 0;
+    for (int i = 0; i < kW; ++i) {
+      uint32_t par = 0;
 #pragma unroll
-      for (int j = 0; j < D; ++j) p ^= (nib(b.row[j], k) < (uint32_t)a.half) ? 1u : 0u;
-      par |= p << k;
+      for (int k = 0; k < 8; ++k) {
+        uint32_t p = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) p ^= (nib(b.row[j][i], k) < (uint32_t)a.half) ? 1u : 0u;
+        par |= p << k;
+      }
+      if (par & valid_mask8(a.B - b.cwb - 8 * i)) unsat = true;
     }
-    if (par & valid_mask8(a.B - b.cwb)) unsat = true;
   }
-  if constexpr (D == 2) {
-    if (a.match) {
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        uint32_t t0[4], t1[4];
+  for (int i = 0; i < kW; ++i) {
+    uint32_t in[D], o[D];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          t0[s] = lds[(nib(b.row[1], 4 * g + s) << 9) + lane4 + fbase];
-          t1[s] = lds[(nib(b.row[0], 4 * g + s) << 9) + lane4 + fbase];
+    for (int j = 0; j < D; ++j) {
+      in[j] = b.row[j][i];
+      o[j] = 0;
+    }
+    if constexpr (D == 2) {
+      if (a.match) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          uint32_t t0[4], t1[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            t0[s] = lds[(nib(in[1], 4 * g + s) << 9) + lane4 + fbase];
+            t1[s] = lds[(nib(in[0], 4 * g + s) << 9) + lane4 + fbase];
+          }
+          o[0] |= pack4n(t0, g);
+          o[1] |= pack4n(t1, g);
         }
-        outw[0] |= pack4n(t0, g);
-        outw[1] |= pack4n(t1, g);
+      } else {
+        o[0] = in[1];
+        o[1] = in[0];
       }
     } else {
-      outw[0] = b.row[1];
-      outw[1] = b.row[0];
+      cn_word<D>(lds, lane4, in, fbase, o);
     }
-  } else {
-    auto sb = [&](int l) -> uint32_t { return (l == D - 3) ? fbase : (uint32_t)(l * kTbl); };
-#pragma unroll 1
-    for (int g = 0; g < 2; ++g) {
-      uint32_t q[D][4];
 #pragma unroll
-      for (int j = 1; j < D; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(b.row[j], 4 * g + s), lane4);
-      uint32_t t[4], P[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = nib(b.row[1], 4 * g + s);
-#pragma unroll
-      for (int j = 2; j < D; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
-      outw[0] |= pack4n(t, g);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) P[s] = nib(b.row[0], 4 * g + s);
-#pragma unroll
-      for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = P[s];
-#pragma unroll
-        for (int j = w + 1; j < D; ++j)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
-        outw[w] |= pack4n(t, g);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
-      }
-      outw[D - 1] |= pack4n(P, g);
-    }
+    for (int w = 0; w < D; ++w) outw[w][i] = o[w];
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off) = outw[w];
+  for (int w = 0; w < D; ++w) store_row<kW>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ---------------------------------------------------------------- variable node
@@ -203,56 +270,73 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
 // c and the other inputs (kernels_template_irreg.cl:151-160): step 0 = channel table V_0,
 // step l = V_l; the last step (l = D-2) uses fslot (matching composed). Degree 1 forwards c
 // (:131-136).
+template <int D>
+__device__ __forceinline__ void vn_word(const uint8_t* lds, uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
+                                        uint32_t fbase, uint32_t (&outw)[D]) {
+  auto sb = [&](int l) -> uint32_t { return (l == D - 2) ? fbase : (uint32_t)(l * kTbl); };
+#if IBL_VN_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+  for (int g = 0; g < 2; ++g) {
+    uint32_t q[D][4], c[4], t[4], Q[4];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c[s] = nib(chw, 4 * g + s) << 9;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
+#pragma unroll
+    for (int j = 2; j < D; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+    outw[0] |= pack4n(t, g);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
+#pragma unroll
+    for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) t[s] = Q[s];
+#pragma unroll
+      for (int j = w + 1; j < D; ++j)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+      outw[w] |= pack4n(t, g);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+    }
+    outw[D - 1] |= pack4n(Q, g);
+  }
+}
+
 template <int D, int MAXD>
 __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot) {
-  uint32_t outw[D], trow[D];
+  uint32_t outw[D][kW], trow[D];
 #pragma unroll
-  for (int w = 0; w < D; ++w) {
-    trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
-    outw[w] = 0;
-  }
-  if constexpr (D == 1) {
-    outw[0] = b.chw;
-  } else {
-    const uint32_t fbase = (uint32_t)fslot * kTbl;
-    auto sb = [&](int l) -> uint32_t { return (l == D - 2) ? fbase : (uint32_t)(l * kTbl); };
-#pragma unroll 1
-    for (int g = 0; g < 2; ++g) {
-      uint32_t q[D][4], c[4], t[4], Q[4];
+  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
+  const uint32_t fbase = (uint32_t)fslot * kTbl;
 #pragma unroll
-      for (int j = 0; j < D; ++j)
+  for (int i = 0; i < kW; ++i) {
+    if constexpr (D == 1) {
+      outw[0][i] = b.chw[i];
+    } else {
+      uint32_t in[D], o[D];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(b.row[j], 4 * g + s), lane4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) c[s] = nib(b.chw, 4 * g + s) << 9;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
-#pragma unroll
-      for (int j = 2; j < D; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
-      outw[0] |= pack4n(t, g);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
-#pragma unroll
-      for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = Q[s];
-#pragma unroll
-        for (int j = w + 1; j < D; ++j)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
-        outw[w] |= pack4n(t, g);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+      for (int j = 0; j < D; ++j) {
+        in[j] = b.row[j][i];
+        o[j] = 0;
       }
-      outw[D - 1] |= pack4n(Q, g);
+      vn_word<D>(lds, lane4, in, b.chw[i], fbase, o);
+#pragma unroll
+      for (int w = 0; w < D; ++w) outw[w][i] = o[w];
     }
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w)
-    *reinterpret_cast<uint32_t*>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off) = outw[w];
+  for (int w = 0; w < D; ++w) store_row<kW>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ------------------------------------------------------------- decision output
@@ -308,7 +392,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds,
 #define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
 
-// Persistent wave loop shared by the CN and VN passes: items (node, 256-codeword chunk) are dealt
+// Persistent wave loop shared by the CN and VN passes: items (node, kChunkIB-codeword chunk) are dealt
 // round-robin to the grid's waves; each iteration prefetches the next item, then computes the
 // current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch).
 template <int MAXD, bool VN, bool GATHER>
@@ -396,8 +480,8 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
     const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
     const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
     const int d = a.deg[node], st = a.start[node];
-    const uint32_t off = (uint32_t)(chunk * (kChunkN / 2) + lane * 4);
-    const int cwb = chunk * kChunkN + lane * 8;
+    const uint32_t off = (uint32_t)(chunk * (kChunkDec / 2) + lane * 4);
+    const int cwb = chunk * kChunkDec + lane * 8;
     if (cwb >= a.B) continue;
     switch (d) {
       case 1: dec_item<1>(a, lds, lane4, node, st, off, cwb); break;

@@ -20,6 +20,12 @@ for s in $STEPS; do
     bench)
       timeout -k 10 400 python $R/bench.py > $O/bench.json 2> $O/bench.err
       rc=$?; echo "bench rc=$rc" >> $O/summary.txt; crash $rc bench;;
+    ab)
+      # A/B the kernel variants built by tools/variants.py (AB_VARIANTS="w1 w2 ...")
+      for v in ${AB_VARIANTS:-w1 w2}; do
+        IBLDPC_LIB=$R/informationbottleneckdecodingldpc_amd/variants/libibldpc_$v.so timeout -k 10 300 python $R/bench.py --no-cpu-baseline ${AB_ARGS:-} > $O/ab_$v.json 2> $O/ab_$v.err
+        rc=$?; echo "ab $v rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['avg_ms'], d['decoded_bit_errors'])" $O/ab_$v.json 2>/dev/null)" >> $O/summary.txt; crash $rc ab_$v
+      done;;
     benchfloat)
       for k in minsum bp; do
         timeout -k 10 400 python $R/bench.py --kind $k --no-cpu-baseline --steps 3 > $O/bench_$k.json 2> $O/bench_$k.err
