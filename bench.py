@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--ebn0", type=float, default=0.6)
     p.add_argument("--kind", choices=["ib", "minsum", "bp"], default="ib")
     p.add_argument("--no-match", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=64)
+    p.add_argument("--cpu-sample", type=int, default=448, help="codewords of the CPU-baseline sample (~15 s on 16 host threads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()

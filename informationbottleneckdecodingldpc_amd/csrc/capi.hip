@@ -468,7 +468,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
   const bool early = early_stop != 0 && I > 1;
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
   if (h->fast) {
-    const int nchunks = (B + kChunkIB - 1) / kChunkIB;
+    const int ccn = ib_fast_chunk(h->CM), cvn = ib_fast_chunk(h->VM);
     const int ldbb = h->ldb / 2;
     HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     IbFastArgs cn{}, vn{};
@@ -476,7 +476,8 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin;
     vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
-    cn.nchunks = vn.nchunks = nchunks;
+    cn.nchunks = (B + ccn - 1) / ccn;
+    vn.nchunks = (B + cvn - 1) / cvn;
     cn.ldb = vn.ldb = ldbb;
     cn.B = vn.B = B;
     cn.half = vn.half = h->T / 2;

@@ -17,7 +17,7 @@ constexpr int kWave = 64;
 constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, fp64: 2x2)
 // IB fast path: 4-bit messages; a lane owns IBL_W dwords (8*IBL_W codewords) of each edge row
 #ifndef IBL_W
-#define IBL_W 1
+#define IBL_W 2
 #endif
 constexpr int kW = IBL_W;
 constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
@@ -118,6 +118,7 @@ hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8
 hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s);
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
+int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for this max degree
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu);
 hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);

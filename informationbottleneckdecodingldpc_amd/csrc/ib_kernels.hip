@@ -53,8 +53,8 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
 }
 
 // Fast-path message format: T <= 16, so every message is a 4-bit nibble; an edge row stores
-// codeword c in nibble (c & 1) of byte c/2. A lane owns 8*kW consecutive codewords = kW dwords of
-// each row, a wave item = one node x kChunkIB codewords (256*kW-B row segments per wave).
+// codeword c in nibble (c & 1) of byte c/2. A lane owns 8*W consecutive codewords = W dwords of
+// each row (W = rowW<MAXD>()), a wave item = one node x 512*W codewords (256*W-B row segments).
 __device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
 
 __device__ __forceinline__ uint32_t valid_mask8(int remaining) {
@@ -92,11 +92,19 @@ __device__ __forceinline__ void store_row(uint8_t* p, const uint32_t (&r)[W]) {
 // A wave item's inputs, fetched one item ahead of its computation (register double buffer):
 // the row loads of item k+1 are issued before item k is computed, so HBM latency overlaps the
 // lookups and the waits never cover the previous item's stores.
+// Dwords per lane and row: kW for the MAXD=8 bodies; the MAXD=16 bodies already use every VGPR a
+// 512-thread block allows and keep one dword (8 codewords) per lane.
+template <int MAXD>
+constexpr int rowW() { return MAXD <= 8 ? kW : 1; }
+template <int MAXD>
+constexpr int chunkOf() { return 512 * rowW<MAXD>(); }
+
 template <int MAXD>
 struct ItemBuf {
-  uint32_t row[MAXD][kW];  // 8*kW packed 4-bit messages (codewords cwb..) of each input row
+  static constexpr int W = rowW<MAXD>();
+  uint32_t row[MAXD][W];  // 8*W packed 4-bit messages (codewords cwb..) of each input row
   uint32_t tgv;            // lane j < d holds the destination row tgt[st + j] of output edge j
-  uint32_t chw[kW];        // channel values (VN) of the same codewords
+  uint32_t chw[W];         // channel values (VN) of the same codewords
   int d, st, node;
   uint32_t off;            // byte offset of this lane's words in a row
   int cwb;                 // first codeword of this lane
@@ -109,21 +117,22 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.node = node;
   b.d = sload(a.deg, node);
   b.st = sload(a.start, node);
-  b.off = (uint32_t)(chunk * (kChunkIB / 2) + lane * 4 * kW);
-  b.cwb = chunk * kChunkIB + lane * 8 * kW;
+  constexpr int W = rowW<MAXD>();
+  b.off = (uint32_t)(chunk * (chunkOf<MAXD>() / 2) + lane * 4 * W);
+  b.cwb = chunk * chunkOf<MAXD>() + lane * 8 * W;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    load_row<kW>(row + b.off, b.row[j]);
+    load_row<W>(row + b.off, b.row[j]);
   }
   if (VN) {
-    load_row<kW>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
+    load_row<W>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
   } else {
 #pragma unroll
-    for (int i = 0; i < kW; ++i) b.chw[i] = 0;
+    for (int i = 0; i < W; ++i) b.chw[i] = 0;
   }
   // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
   // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
@@ -135,12 +144,13 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
 // path (switch cases, default) leaves these registers "possibly pending" at a merge point.
 template <int MAXD>
 __device__ __forceinline__ void settle(const ItemBuf<MAXD>& b) {
+  constexpr int W = ItemBuf<MAXD>::W;
 #pragma unroll
   for (int j = 0; j < MAXD; ++j)
 #pragma unroll
-    for (int i = 0; i < kW; ++i) asm volatile("" ::"v"(b.row[j][i]));
+    for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.row[j][i]));
 #pragma unroll
-  for (int i = 0; i < kW; ++i) asm volatile("" ::"v"(b.chw[i]));
+  for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.chw[i]));
   asm volatile("" ::"v"(b.tgv));
 }
 
@@ -208,17 +218,18 @@ __device__ __forceinline__ void cn_word(const uint8_t* lds, uint32_t lane4, cons
 template <int D, int MAXD>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
-  uint32_t outw[D][kW], trow[D];
+  constexpr int W = ItemBuf<MAXD>::W;
+  uint32_t outw[D][W], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) {
     trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
 #pragma unroll
-    for (int i = 0; i < kW; ++i) outw[w][i] = 0;
+    for (int i = 0; i < W; ++i) outw[w][i] = 0;
   }
   const uint32_t fbase = (uint32_t)fslot * kTbl;
   if (do_par) {
 #pragma unroll
-    for (int i = 0; i < kW; ++i) {
+    for (int i = 0; i < W; ++i) {
       uint32_t par = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -231,7 +242,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
     }
   }
 #pragma unroll
-  for (int i = 0; i < kW; ++i) {
+  for (int i = 0; i < W; ++i) {
     uint32_t in[D], o[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -262,7 +273,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
     for (int w = 0; w < D; ++w) outw[w][i] = o[w];
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w) store_row<kW>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ---------------------------------------------------------------- variable node
@@ -315,12 +326,13 @@ __device__ __forceinline__ void vn_word(const uint8_t* lds, uint32_t lane4, cons
 template <int D, int MAXD>
 __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot) {
-  uint32_t outw[D][kW], trow[D];
+  constexpr int W = ItemBuf<MAXD>::W;
+  uint32_t outw[D][W], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   const uint32_t fbase = (uint32_t)fslot * kTbl;
 #pragma unroll
-  for (int i = 0; i < kW; ++i) {
+  for (int i = 0; i < W; ++i) {
     if constexpr (D == 1) {
       outw[0][i] = b.chw[i];
     } else {
@@ -336,7 +348,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* l
     }
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w) store_row<kW>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ------------------------------------------------------------- decision output
@@ -405,7 +417,8 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   const int nitems = a.n_nodes * a.nchunks;
   const bool do_par = !VN && a.unsat != nullptr;
   bool unsat = false;
-  auto compute = [&](const ItemBuf<MAXD>& cur) {
+  // always inlined: an out-of-line body would take the item by reference through scratch
+  auto compute = [&](const ItemBuf<MAXD>& cur) __attribute__((always_inline)) {
     settle(cur);
     if constexpr (VN) {
       switch (cur.d) {
@@ -711,6 +724,7 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
   else hipLaunchKernelGGL(ib_vn_fast<16>, dim3(grid), dim3(block), lds, s, a);
   return hipGetLastError();
 }
+int ib_fast_chunk(int maxd) { return maxd <= 8 ? chunkOf<8>() : chunkOf<16>(); }
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(ib_dec_fast, dim3(grid), dim3(block), lds, s, a);
   return hipGetLastError();

@@ -7,10 +7,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from informationbottleneckdecodingldpc_amd import _build  # noqa: E402
 
 VARIANTS = {
-    "w1": [],
-    "w1u": ["IBL_CN_UNROLL=1"],
+    "w1": ["IBL_W=1"],
+    "w1u": ["IBL_W=1", "IBL_CN_UNROLL=1"],
     "w2": ["IBL_W=2"],
     "w2u": ["IBL_W=2", "IBL_CN_UNROLL=1"],
+    "w4": ["IBL_W=4"],
 }
 
 if __name__ == "__main__":
