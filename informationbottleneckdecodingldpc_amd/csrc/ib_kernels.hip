@@ -33,6 +33,22 @@ namespace ibl {
 typedef __attribute__((address_space(4))) const int32_t cint32;
 __device__ __forceinline__ int32_t sload(const int32_t* p, int i) { return ((cint32*)p)[i]; }
 
+// LDS lookups take a 32-bit LDS byte address. These kernels have no static LDS, so the dynamic
+// array starts at LDS address 0 (checked at kernel entry: lds_at_zero): a lookup is one v_lshl_add
+// (row of t plus the precomputed column term) and one ds_read_u8 whose immediate offset selects
+// the table — adding the link-time base of the extern array would cost a second VALU op.
+typedef __attribute__((address_space(3))) const uint8_t lds8_t;
+// x = row/column part (one v_lshl_add), c = table slot base: x is made opaque so c stays a top-level
+// constant and folds into the DS immediate offset instead of being pre-added per input in VGPRs.
+__device__ __forceinline__ uint32_t lu(uint32_t x, uint32_t c) {
+  asm("" : "+v"(x));
+  return *(lds8_t*)(size_t)(x + c);
+}
+__device__ __forceinline__ uint32_t lds_base(const uint8_t* p) { return (uint32_t)(size_t)(lds8_t*)p; }
+__device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
+  if (lds_base(lds) != 0u) __builtin_trap();  // uniform scalar test; never taken without static LDS
+}
+
 __device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
   return ((m >> 2) << 7) + (m & 3u) + lane4;
 }
@@ -175,9 +191,12 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 // Step l uses LDS slot l, except the last step (l = D-3) which uses fslot (matching composed).
 // One dword of each row = 8 codewords, run as two groups of 4 (4 independent reads per step).
 template <int D>
-__device__ __forceinline__ void cn_word(const uint8_t* lds, uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
+__device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         uint32_t (&outw)[D]) {
-  auto sb = [&](int l) -> uint32_t { return (l == D - 3) ? fbase : (uint32_t)(l * kTbl); };
+  // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
+  auto sb = [&](int j, int l) -> uint32_t {
+    return j == D - 1 ? 0u : (l == D - 3) ? fbase : (uint32_t)(l * kTbl);
+  };
 #if IBL_CN_UNROLL
 #pragma unroll
 #else
@@ -189,13 +208,15 @@ __device__ __forceinline__ void cn_word(const uint8_t* lds, uint32_t lane4, cons
     for (int j = 1; j < D; ++j)
 #pragma unroll
       for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) q[D - 1][s] += fbase;
     uint32_t t[4], P[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) t[s] = nib(in[1], 4 * g + s);
 #pragma unroll
     for (int j = 2; j < D; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+      for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 2));
     outw[0] |= pack4n(t, g);
 #pragma unroll
     for (int s = 0; s < 4; ++s) P[s] = nib(in[0], 4 * g + s);
@@ -206,17 +227,17 @@ __device__ __forceinline__ void cn_word(const uint8_t* lds, uint32_t lane4, cons
 #pragma unroll
       for (int j = w + 1; j < D; ++j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 2)];
+        for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 2));
       outw[w] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) P[s] = lds[(P[s] << 9) + q[w][s] + sb(w - 1)];
+      for (int s = 0; s < 4; ++s) P[s] = lu((P[s] << 9) + q[w][s], sb(w, w - 1));
     }
     outw[D - 1] |= pack4n(P, g);
   }
 }
 
 template <int D, int MAXD>
-__device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
+__device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
   constexpr int W = ItemBuf<MAXD>::W;
   uint32_t outw[D][W], trow[D];
@@ -256,8 +277,8 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
           uint32_t t0[4], t1[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            t0[s] = lds[(nib(in[1], 4 * g + s) << 9) + lane4 + fbase];
-            t1[s] = lds[(nib(in[0], 4 * g + s) << 9) + lane4 + fbase];
+            t0[s] = lu((nib(in[1], 4 * g + s) << 9) + lane4, fbase);
+            t1[s] = lu((nib(in[0], 4 * g + s) << 9) + lane4, fbase);
           }
           o[0] |= pack4n(t0, g);
           o[1] |= pack4n(t1, g);
@@ -267,7 +288,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
         o[1] = in[0];
       }
     } else {
-      cn_word<D>(lds, lane4, in, fbase, o);
+      cn_word<D>(lane4, in, fbase, o);
     }
 #pragma unroll
     for (int w = 0; w < D; ++w) outw[w][i] = o[w];
@@ -282,9 +303,12 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, const uint8_t* l
 // step l = V_l; the last step (l = D-2) uses fslot (matching composed). Degree 1 forwards c
 // (:131-136).
 template <int D>
-__device__ __forceinline__ void vn_word(const uint8_t* lds, uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
+__device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, uint32_t (&outw)[D]) {
-  auto sb = [&](int l) -> uint32_t { return (l == D - 2) ? fbase : (uint32_t)(l * kTbl); };
+  // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
+  auto sb = [&](int j, int l) -> uint32_t {
+    return j == D - 1 ? 0u : (l == D - 2) ? fbase : (uint32_t)(l * kTbl);
+  };
 #if IBL_VN_UNROLL
 #pragma unroll
 #else
@@ -297,16 +321,18 @@ __device__ __forceinline__ void vn_word(const uint8_t* lds, uint32_t lane4, cons
 #pragma unroll
       for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
 #pragma unroll
+    for (int s = 0; s < 4; ++s) q[D - 1][s] += fbase;
+#pragma unroll
     for (int s = 0; s < 4; ++s) c[s] = nib(chw, 4 * g + s) << 9;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = lds[c[s] + q[1][s] + sb(0)];
+    for (int s = 0; s < 4; ++s) t[s] = lu(c[s] + q[1][s], sb(1, 0));
 #pragma unroll
     for (int j = 2; j < D; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+      for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 1));
     outw[0] |= pack4n(t, g);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) Q[s] = lds[c[s] + q[0][s] + sb(0)];
+    for (int s = 0; s < 4; ++s) Q[s] = lu(c[s] + q[0][s], sb(0, 0));
 #pragma unroll
     for (int w = 1; w <= D - 2; ++w) {
 #pragma unroll
@@ -314,17 +340,17 @@ __device__ __forceinline__ void vn_word(const uint8_t* lds, uint32_t lane4, cons
 #pragma unroll
       for (int j = w + 1; j < D; ++j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lds[(t[s] << 9) + q[j][s] + sb(j - 1)];
+        for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 1));
       outw[w] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) Q[s] = lds[(Q[s] << 9) + q[w][s] + sb(w)];
+      for (int s = 0; s < 4; ++s) Q[s] = lu((Q[s] << 9) + q[w][s], sb(w, w));
     }
     outw[D - 1] |= pack4n(Q, g);
   }
 }
 
 template <int D, int MAXD>
-__device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* lds, uint32_t lane4,
+__device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4,
                                            const ItemBuf<MAXD>& b, int fslot) {
   constexpr int W = ItemBuf<MAXD>::W;
   uint32_t outw[D][W], trow[D];
@@ -342,7 +368,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, const uint8_t* l
         in[j] = b.row[j][i];
         o[j] = 0;
       }
-      vn_word<D>(lds, lane4, in, b.chw[i], fbase, o);
+      vn_word<D>(lane4, in, b.chw[i], fbase, o);
 #pragma unroll
       for (int w = 0; w < D; ++w) outw[w][i] = o[w];
     }
@@ -379,7 +405,7 @@ __device__ __forceinline__ void store4(void* out, int dtype, size_t row_off, int
 }
 
 template <int D>
-__device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds, uint32_t lane4, int node,
+__device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int node,
                                          int st, uint32_t off, int cwb) {
   uint32_t inw[D];
 #pragma unroll
@@ -391,9 +417,9 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds,
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int k = 4 * g + s;
-      uint32_t Q = lds[(nib(cw, k) << 9) + qidx(nib(inw[0], k), lane4)];
+      uint32_t Q = lu((nib(cw, k) << 9) + qidx(nib(inw[0], k), lane4), 0);
 #pragma unroll
-      for (int l = 1; l < D; ++l) Q = lds[(Q << 9) + qidx(nib(inw[l], k), lane4) + l * kTbl];
+      for (int l = 1; l < D; ++l) Q = lu((Q << 9) + qidx(nib(inw[l], k), lane4), l * kTbl);
       packed |= Q << (8 * s);
     }
     store4(a.out, a.out_dtype, (size_t)node * a.B, cwb + 4 * g, a.B, a.aligned != 0, packed);
@@ -410,7 +436,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, const uint8_t* lds,
 template <int MAXD, bool VN, bool GATHER>
 __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
-  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
   const int wpb = blockDim.x >> 6;
   // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
@@ -422,15 +448,15 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
     settle(cur);
     if constexpr (VN) {
       switch (cur.d) {
-        case 1: vn_compute<1, MAXD>(a, lds, lane4, cur, 0); break;
-#define X(D) case D: if constexpr (D <= MAXD) vn_compute<D, MAXD>(a, lds, lane4, cur, a.fslot[D]); break;
+        case 1: vn_compute<1, MAXD>(a, lane4, cur, 0); break;
+#define X(D) case D: if constexpr (D <= MAXD) vn_compute<D, MAXD>(a, lane4, cur, a.fslot[D]); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
       }
     } else {
       switch (cur.d) {
-#define X(D) case D: if constexpr (D <= MAXD) cn_compute<D, MAXD>(a, lds, lane4, cur, a.fslot[D], do_par, unsat); break;
+#define X(D) case D: if constexpr (D <= MAXD) cn_compute<D, MAXD>(a, lane4, cur, a.fslot[D], do_par, unsat); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
@@ -460,20 +486,25 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 }
 
 // MAXD=16 bodies need more than the 128 VGPRs a 1024-thread block allows: cap those at 512
-// threads (256 VGPRs, no scratch spill); the MAXD=8 bodies fit 1024-thread blocks.
+// threads (256 VGPRs, no scratch spill); the MAXD=8 bodies fit 1024-thread blocks at W <= 2.
+#ifndef IBL_LB8
+#define IBL_LB8 1024
+#endif
 template <int MAXD, bool GATHER>
-__global__ __launch_bounds__(MAXD <= 8 ? 1024 : 512) void ib_cn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
+  lds_at_zero(lds);
   stage_tables(lds, a.img, a.nt);
   __syncthreads();
   ib_pass<MAXD, false, GATHER>(a, lds);
 }
 
 template <int MAXD>
-__global__ __launch_bounds__(MAXD <= 8 ? 1024 : 512) void ib_vn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512) void ib_vn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
+  lds_at_zero(lds);
   stage_tables(lds, a.img, a.nt);
   __syncthreads();
   ib_pass<MAXD, true, false>(a, lds);
@@ -483,9 +514,10 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
+  lds_at_zero(lds);
   stage_tables(lds, a.img + (size_t)L * a.nt * 64, a.nt);
   __syncthreads();
-  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
   const int wpb = blockDim.x >> 6;
   const int gw = blockIdx.x * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
   const int nitems = a.n_nodes * a.nchunks;
@@ -497,8 +529,8 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
     const int cwb = chunk * kChunkDec + lane * 8;
     if (cwb >= a.B) continue;
     switch (d) {
-      case 1: dec_item<1>(a, lds, lane4, node, st, off, cwb); break;
-#define X(D) case D: dec_item<D>(a, lds, lane4, node, st, off, cwb); break;
+      case 1: dec_item<1>(a, lane4, node, st, off, cwb); break;
+#define X(D) case D: dec_item<D>(a, lane4, node, st, off, cwb); break;
       IBL_DEG_CASES(X)
 #undef X
       default: break;
@@ -741,6 +773,10 @@ hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* bl
                              : (const void*)ib_dec_fast;
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  hipFuncAttributes fa;
+  e = hipFuncGetAttributes(&fa, f);
+  if (e != hipSuccess) return e;
+  if (block > fa.maxThreadsPerBlock) return hipErrorInvalidValue;  // above the kernel's launch bounds
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, block, lds);
 }
 static int gen_grid(int n_nodes, int B) {

@@ -10,8 +10,9 @@ VARIANTS = {
     "w1": ["IBL_W=1"],
     "w1u": ["IBL_W=1", "IBL_CN_UNROLL=1"],
     "w2": ["IBL_W=2"],
-    "w2u": ["IBL_W=2", "IBL_CN_UNROLL=1"],
-    "w4": ["IBL_W=4"],
+    "w2u": ["IBL_W=2", "IBL_CN_UNROLL=1", "IBL_LB8=512"],
+    "w4": ["IBL_W=4", "IBL_LB8=512"],
+    "w2b": ["IBL_W=2", "IBL_LB8=512"],
 }
 
 if __name__ == "__main__":
