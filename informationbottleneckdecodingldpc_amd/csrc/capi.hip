@@ -70,7 +70,30 @@ struct ibl_graph {
   std::vector<int32_t> h_cn_deg, h_vn_deg;
   int32_t *cn_start = nullptr, *cn_deg = nullptr, *tgt_cn = nullptr;
   int32_t *vn_start = nullptr, *vn_deg = nullptr, *tgt_vn = nullptr, *csr_cols = nullptr;
+  // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable)
+  int32_t *cn_info = nullptr, *vn_info = nullptr;
+  int32_t cn_heavy = 0, vn_heavy = 0;
 };
+
+namespace {
+std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::vector<int32_t>& deg, int32_t* heavy) {
+  const int32_t n = (int32_t)deg.size();
+  std::vector<int32_t> idx(n);
+  for (int32_t i = 0; i < n; ++i) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
+  std::vector<int32_t> info((size_t)n * 4);
+  *heavy = 0;
+  for (int32_t p = 0; p < n; ++p) {
+    const int32_t v = idx[p];
+    info[4 * (size_t)p] = v;
+    info[4 * (size_t)p + 1] = start[v];
+    info[4 * (size_t)p + 2] = deg[v];
+    info[4 * (size_t)p + 3] = 0;
+    if (deg[v] > kLightD) ++*heavy;
+  }
+  return info;
+}
+}  // namespace
 
 // HIP-event timing of the CN / VN launches (benchmark only).
 struct KTimer {
@@ -228,7 +251,9 @@ int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int3
   if ((rc = dupload(&g->cn_start, cs.data(), n_c)) || (rc = dupload(&g->cn_deg, cd.data(), n_c)) ||
       (rc = dupload(&g->tgt_cn, tc.data(), E)) || (rc = dupload(&g->vn_start, vs.data(), n_v)) ||
       (rc = dupload(&g->vn_deg, vd.data(), n_v)) || (rc = dupload(&g->tgt_vn, tv.data(), E)) ||
-      (rc = dupload(&g->csr_cols, cols, E))) {
+      (rc = dupload(&g->csr_cols, cols, E)) ||
+      (rc = dupload(&g->cn_info, work_order(cs, cd, &g->cn_heavy).data(), (size_t)n_c * 4)) ||
+      (rc = dupload(&g->vn_info, work_order(vs, vd, &g->vn_heavy).data(), (size_t)n_v * 4))) {
     ibl_graph_destroy(g);
     return rc;
   }
@@ -251,6 +276,7 @@ void ibl_graph_destroy(ibl_graph* g) {
   (void)hipSetDevice(g->device);
   dfree(g->cn_start); dfree(g->cn_deg); dfree(g->tgt_cn);
   dfree(g->vn_start); dfree(g->vn_deg); dfree(g->tgt_vn); dfree(g->csr_cols);
+  dfree(g->cn_info); dfree(g->vn_info);
   delete g;
 }
 
@@ -473,9 +499,10 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     IbFastArgs cn{}, vn{};
     cn.ch8 = vn.ch8 = h->ch8;
-    cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.out = h->vin;
-    vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
+    cn.info = g->cn_info; cn.tgt = g->tgt_cn; cn.out = h->vin;
+    vn.info = g->vn_info; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.n_heavy = g->cn_heavy; vn.n_heavy = g->vn_heavy;
     cn.nchunks = (B + ccn - 1) / ccn;
     vn.nchunks = (B + cvn - 1) / cvn;
     cn.ldb = vn.ldb = ldbb;

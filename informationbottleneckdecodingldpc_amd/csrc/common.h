@@ -24,7 +24,8 @@ constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
 constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item
 constexpr int kTbl = 8192;        // one IB lookup table replicated over the 32 LDS banks
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
-constexpr int kMaxD = 16;         // largest node degree with an unrolled fast-path body
+constexpr int kMaxD = 16;
+constexpr int kLightD = 4;        // nodes up to this degree run with a 4-row item buffer         // largest node degree with an unrolled fast-path body
 constexpr int kShards = 64;       // early-stop flag words per iteration (one wave load)
 constexpr int kLdsBytes = 160 * 1024;
 
@@ -35,8 +36,7 @@ struct IbFastArgs {
   const uint8_t* in;        // own-order inbox (nullptr for CN pass 0: inputs gathered from ch8)
   uint8_t* out;             // other-order inbox
   const uint8_t* ch8;       // staged channel cluster ids: 4-bit nibbles [N][ldb bytes]
-  const int32_t* start;     // node -> first own-order edge
-  const int32_t* deg;       // node degree
+  const int32_t* info;      // per position (heaviest node first): {node, first own-order edge, degree, 0}
   const int32_t* tgt;       // own-order edge -> other-order row
   const int32_t* gather;    // CN pass 0: csr_cols (edge -> variable node); else nullptr
   const uint32_t* img;      // this pass's tables: nt x 64 dwords (256 entries, t*16+m)
@@ -45,6 +45,7 @@ struct IbFastArgs {
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
   int32_t nt;               // tables staged in LDS
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
+  int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
 };
 
 struct IbDecArgs {

@@ -114,11 +114,12 @@ template <int MAXD>
 constexpr int rowW() { return MAXD <= 8 ? kW : 1; }
 template <int MAXD>
 constexpr int chunkOf() { return 512 * rowW<MAXD>(); }
+static_assert(kLightD <= 8, "light item buffers must fit the MAXD=8 bodies");
 
-template <int MAXD>
+template <int MAXD, int W_ = rowW<MAXD>()>
 struct ItemBuf {
-  static constexpr int W = rowW<MAXD>();
-  uint32_t row[MAXD][W];  // 8*W packed 4-bit messages (codewords cwb..) of each input row
+  static constexpr int kMax = MAXD, W = W_;
+  uint32_t row[MAXD][W];   // 8*W packed 4-bit messages (codewords cwb..) of each input row
   uint32_t tgv;            // lane j < d holds the destination row tgt[st + j] of output edge j
   uint32_t chw[W];         // channel values (VN) of the same codewords
   int d, st, node;
@@ -126,16 +127,17 @@ struct ItemBuf {
   int cwb;                 // first codeword of this lane
 };
 
-template <int MAXD, bool VN, bool GATHER>
-__device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, ItemBuf<MAXD>& b) {
-  const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
-  const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+template <class Buf, bool VN, bool GATHER>
+__device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, Buf& b) {
+  constexpr int W = Buf::W, MAXD = Buf::kMax;
+  const int pos = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+  const int chunk = __builtin_amdgcn_readfirstlane(item - pos * a.nchunks);
+  const int node = sload(a.info, 4 * pos);
   b.node = node;
-  b.d = sload(a.deg, node);
-  b.st = sload(a.start, node);
-  constexpr int W = rowW<MAXD>();
-  b.off = (uint32_t)(chunk * (chunkOf<MAXD>() / 2) + lane * 4 * W);
-  b.cwb = chunk * chunkOf<MAXD>() + lane * 8 * W;
+  b.st = sload(a.info, 4 * pos + 1);
+  b.d = sload(a.info, 4 * pos + 2);
+  b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * W);
+  b.cwb = chunk * (512 * W) + lane * 8 * W;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
@@ -158,11 +160,11 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
 // Empty asm that consumes every register of a fetched item: the compiler inserts ONE counted
 // vmcnt wait for exactly this item's loads here (younger prefetches stay in flight), and no later
 // path (switch cases, default) leaves these registers "possibly pending" at a merge point.
-template <int MAXD>
-__device__ __forceinline__ void settle(const ItemBuf<MAXD>& b) {
-  constexpr int W = ItemBuf<MAXD>::W;
+template <class Buf>
+__device__ __forceinline__ void settle(const Buf& b) {
+  constexpr int W = Buf::W;
 #pragma unroll
-  for (int j = 0; j < MAXD; ++j)
+  for (int j = 0; j < Buf::kMax; ++j)
 #pragma unroll
     for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.row[j][i]));
 #pragma unroll
@@ -236,10 +238,10 @@ __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D],
   }
 }
 
-template <int D, int MAXD>
-__device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4,
-                                           const ItemBuf<MAXD>& b, int fslot, bool do_par, bool& unsat) {
-  constexpr int W = ItemBuf<MAXD>::W;
+template <int D, class Buf>
+__device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, const Buf& b, int fslot, bool do_par,
+                                           bool& unsat) {
+  constexpr int W = Buf::W;
   uint32_t outw[D][W], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) {
@@ -349,10 +351,9 @@ __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D],
   }
 }
 
-template <int D, int MAXD>
-__device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4,
-                                           const ItemBuf<MAXD>& b, int fslot) {
-  constexpr int W = ItemBuf<MAXD>::W;
+template <int D, class Buf>
+__device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, const Buf& b, int fslot) {
+  constexpr int W = Buf::W;
   uint32_t outw[D][W], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
@@ -430,33 +431,28 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 #define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
 
-// Persistent wave loop shared by the CN and VN passes: items (node, kChunkIB-codeword chunk) are dealt
+// Persistent wave loop shared by the CN and VN passes: items (position, chunk) are dealt
 // round-robin to the grid's waves; each iteration prefetches the next item, then computes the
-// current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch).
-template <int MAXD, bool VN, bool GATHER>
-__device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
-  const int wpb = blockDim.x >> 6;
-  // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
-  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
-  const int nitems = a.n_nodes * a.nchunks;
-  const bool do_par = !VN && a.unsat != nullptr;
-  bool unsat = false;
+// current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch). Positions are
+// heaviest-first: [0, n_heavy) run with a MAXD-row item buffer, the rest with a kLightD-row one
+// (a degree-2 node then issues 4 row loads, not MAXD).
+template <class Buf, bool VN, bool GATHER, int DLO>
+__device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, int lane, int first, int end, int nw,
+                                         bool do_par, bool& unsat) {
   // always inlined: an out-of-line body would take the item by reference through scratch
-  auto compute = [&](const ItemBuf<MAXD>& cur) __attribute__((always_inline)) {
+  auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
     settle(cur);
     if constexpr (VN) {
       switch (cur.d) {
-        case 1: vn_compute<1, MAXD>(a, lane4, cur, 0); break;
-#define X(D) case D: if constexpr (D <= MAXD) vn_compute<D, MAXD>(a, lane4, cur, a.fslot[D]); break;
+        case 1: if constexpr (DLO < 1) vn_compute<1>(a, lane4, cur, 0); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) vn_compute<D>(a, lane4, cur, a.fslot[D]); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
       }
     } else {
       switch (cur.d) {
-#define X(D) case D: if constexpr (D <= MAXD) cn_compute<D, MAXD>(a, lane4, cur, a.fslot[D], do_par, unsat); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D>(a, lane4, cur, a.fslot[D], do_par, unsat); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
@@ -466,22 +462,37 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   // ping-pong buffers (no register copies: a copy would wait for the prefetched loads). The
   // prefetch is unconditional (clamped to the last item) so the control flow stays straight-line
   // and the compiler's wait for the current item leaves the next item's loads in flight.
-  ItemBuf<MAXD> A, Bb;
-  int item = gw;
-  if (item >= nitems) return;
-  fetch_item<MAXD, VN, GATHER>(a, item, lane, A);
+  Buf A, Bb;
+  int item = first;
+  if (item >= end) return;
+  fetch_item<Buf, VN, GATHER>(a, item, lane, A);
   for (;;) {
     int next = item + nw;
-    fetch_item<MAXD, VN, GATHER>(a, min(next, nitems - 1), lane, Bb);
+    fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb);
     compute(A);
-    if (next >= nitems) break;
+    if (next >= end) break;
     item = next;
     next = item + nw;
-    fetch_item<MAXD, VN, GATHER>(a, min(next, nitems - 1), lane, A);
+    fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A);
     compute(Bb);
-    if (next >= nitems) break;
+    if (next >= end) break;
     item = next;
   }
+}
+
+template <int MAXD, bool VN, bool GATHER>
+__device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
+  const int wpb = blockDim.x >> 6;
+  // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
+  const int heavy_end = a.n_heavy * a.nchunks, nitems = a.n_nodes * a.nchunks;
+  const bool do_par = !VN && a.unsat != nullptr;
+  bool unsat = false;
+  constexpr int W = rowW<MAXD>();
+  ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane, gw, heavy_end, nw, do_par, unsat);
+  ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane, heavy_end + gw, nitems, nw, do_par, unsat);
   if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
 }
 
