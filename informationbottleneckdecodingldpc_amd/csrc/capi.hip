@@ -595,9 +595,9 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess)
     return bail(fail(IBL_EHIP, "hipMemset failed"));
   int bpc = 0;
-  if (fl_occupancy(0, kind, precision, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  if (fl_occupancy(0, kind, precision, g->dcm, &bpc) != hipSuccess || bpc < 1) bpc = 4;
   h->grid_cn = bpc * g->num_cus;
-  if (fl_occupancy(1, kind, precision, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 4;
   h->grid_vn = bpc * g->num_cus;
   *out = h;
   return IBL_OK;
@@ -643,10 +643,10 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     cn.out = vb;
     cn.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
     cn.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn(cn, h->kind, h->prec, h->grid_cn, s); }));
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn(cn, h->kind, h->prec, h->g->dcm, h->grid_cn, s); }));
     vn.in = vb;
     vn.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-    HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn(vn, h->prec, h->grid_vn, s); }));
+    HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn(vn, h->prec, h->g->dvm, h->grid_vn, s); }));
   }
   HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
   FlDecArgs dc{};

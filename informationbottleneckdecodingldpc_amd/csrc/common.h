@@ -131,9 +131,9 @@ hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int
 
 hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s);
 hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s);
-hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int grid, hipStream_t s);
-hipError_t launch_fl_vn(const FlArgs& a, int prec, int grid, hipStream_t s);
+hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
+hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
-hipError_t fl_occupancy(int which, int kind, int prec, int* blocks_per_cu);
+hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
 
 }  // namespace ibl

@@ -186,7 +186,9 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 
 #define FL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 
-template <int KIND, typename F>
+// MAXD = largest degree with a body in the switch (8 or 16): the registers of the degree-16 bodies
+// would cap every launch's occupancy, so codes with degrees <= 8 get their own instantiation.
+template <int KIND, typename F, int MAXD>
 __global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
   const int lane = threadIdx.x & 63;
   if (!fl_gate(a.gate, lane)) return;
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
     const int cw0 = chunk * CH + lane * CWL;
     const int valid = a.B - cw0;
     switch (d) {
-#define X(D) case D: fl_cn_item<KIND, F, D>(a, st, cw0, do_par, valid, unsat); break;
+#define X(D) case D: if constexpr (D <= MAXD) fl_cn_item<KIND, F, D>(a, st, cw0, do_par, valid, unsat); break;
       FL_DEG_CASES(X)
 #undef X
       default: break;
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
   if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
 }
 
-template <typename F>
+template <typename F, int MAXD>
 __global__ __launch_bounds__(256) void fl_vn(FlArgs a) {
   const int lane = threadIdx.x & 63;
   if (!fl_gate(a.gate, lane)) return;
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(256) void fl_vn(FlArgs a) {
     const int cw0 = chunk * CH + lane * CWL;
     switch (d) {
       case 1: fl_vn_item<F, 1>(a, node, st, cw0); break;
-#define X(D) case D: fl_vn_item<F, D>(a, node, st, cw0); break;
+#define X(D) case D: if constexpr (D <= MAXD) fl_vn_item<F, D>(a, node, st, cw0); break;
       FL_DEG_CASES(X)
 #undef X
       default: break;
@@ -310,21 +312,29 @@ hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int grid, hipStream_t s) {
-  if (prec == kF32) {
-    if (kind == 0) hipLaunchKernelGGL((fl_cn<0, float>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((fl_cn<1, float>), dim3(grid), dim3(256), 0, s, a);
-  } else {
-    if (kind == 0) hipLaunchKernelGGL((fl_cn<0, double>), dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((fl_cn<1, double>), dim3(grid), dim3(256), 0, s, a);
+static const void* fl_kernel(int which, int kind, int prec, int maxd) {
+  const bool f32 = prec == kF32, small = maxd <= 8;
+  if (which == 0) {
+    if (kind == 0)
+      return f32 ? (small ? (const void*)fl_cn<0, float, 8> : (const void*)fl_cn<0, float, 16>)
+                 : (small ? (const void*)fl_cn<0, double, 8> : (const void*)fl_cn<0, double, 16>);
+    return f32 ? (small ? (const void*)fl_cn<1, float, 8> : (const void*)fl_cn<1, float, 16>)
+               : (small ? (const void*)fl_cn<1, double, 8> : (const void*)fl_cn<1, double, 16>);
   }
-  return hipGetLastError();
+  return f32 ? (small ? (const void*)fl_vn<float, 8> : (const void*)fl_vn<float, 16>)
+             : (small ? (const void*)fl_vn<double, 8> : (const void*)fl_vn<double, 16>);
 }
 
-hipError_t launch_fl_vn(const FlArgs& a, int prec, int grid, hipStream_t s) {
-  if (prec == kF32) hipLaunchKernelGGL(fl_vn<float>, dim3(grid), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(fl_vn<double>, dim3(grid), dim3(256), 0, s, a);
-  return hipGetLastError();
+hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s) {
+  FlArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_kernel(0, kind, prec, maxd), dim3(grid), dim3(256), p, 0, s);
+}
+
+hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s) {
+  FlArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(256), p, 0, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
@@ -333,15 +343,8 @@ hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) 
   return hipGetLastError();
 }
 
-hipError_t fl_occupancy(int which, int kind, int prec, int* blocks_per_cu) {
-  const void* f;
-  if (which == 0) {
-    f = prec == kF32 ? (kind == 0 ? (const void*)fl_cn<0, float> : (const void*)fl_cn<1, float>)
-                     : (kind == 0 ? (const void*)fl_cn<0, double> : (const void*)fl_cn<1, double>);
-  } else {
-    f = prec == kF32 ? (const void*)fl_vn<float> : (const void*)fl_vn<double>;
-  }
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
+hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fl_kernel(which, kind, prec, maxd), 256, 0);
 }
 
 }  // namespace ibl
