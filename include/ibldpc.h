@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define IBL_VERSION 1
+#define IBL_VERSION 2
 
 enum { IBL_OK = 0, IBL_EINVAL = -1, IBL_EHIP = -2, IBL_ENOMEM = -3, IBL_EUNSUPPORTED = -4 };
 enum { IBL_U8 = 1, IBL_I32 = 2, IBL_F32 = 3, IBL_F64 = 4 };
@@ -135,6 +135,22 @@ int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_launches, dou
  */
 int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
                     int64_t* d_count, void* stream);
+
+/* Channel generation on the device — replaces
+ * AWGN_Channel_Transmission/AWGN_Quantizer_BPSK.py quantize_direct_OpenCL (:216-240) and
+ * quantize_direct_OpenCL_LLR (:242-260) + kernels_quanti_template.cl (:1-52), which sample
+ * u ~ U[0,1) with np.random.rand on the host and upload N*B float64 per batch.
+ *
+ * Writes out[r][b] (row stride ld elements, r < n, b < B) for the quantiser with cluster CDF
+ * cdf[0..T] (host array, cdf[0] = 0, T <= 64): t = #{w in 1..T : u > cdf[w]} clamped to T-1,
+ * mirrored to T-1-t where d_bits[r*B+b] is 1 (d_bits may be NULL: all-zero codeword).
+ * out_dtype IBL_U8 / IBL_I32 store t; IBL_F32 / IBL_F64 store llr[t] (host array of T).
+ * u for element i = r*B+b is the i-th output x of numpy's np.random.Philox(counter=offset,
+ * key=seed) stream as (x >> 11) * 2^-53; a batch consumes ceil(n*B/4) counter blocks, so the
+ * next batch (or GPU) uses offset += ceil(n*B/4).
+ */
+int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t seed, uint64_t offset, int32_t n,
+                       int32_t B, const uint8_t* d_bits, void* d_out, int32_t out_dtype, int64_t ld, void* stream);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ EXPORTS = [
     "ibl_ib_create", "ibl_ib_path", "ibl_ib_decode", "ibl_ib_destroy",
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
     "ibl_ib_timing", "ibl_ib_timing_read", "ibl_float_timing", "ibl_float_timing_read",
+    "ibl_channel_sample",
 ]
 
 
@@ -75,6 +76,9 @@ def load():
         getattr(L, nm).argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]
     L.ibl_count_below.argtypes = [_vp, _i32, _i64, _i32, _i64, ctypes.c_double, _vp, _vp]
+    _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+    L.ibl_channel_sample.argtypes = [_dp, _i32, _vp, ctypes.c_uint64, ctypes.c_uint64, _i32, _i32, _vp, _vp,
+                                     _i32, _i64, _vp]
     for name in EXPORTS:
         getattr(L, name)
     _lib = L

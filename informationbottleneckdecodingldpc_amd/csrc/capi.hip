@@ -658,6 +658,34 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   return IBL_OK;
 }
 
+int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t seed, uint64_t offset, int32_t n,
+                       int32_t B, const uint8_t* d_bits, void* d_out, int32_t out_dtype, int64_t ld, void* stream) {
+  if (!cdf || !d_out) return fail(IBL_EINVAL, "NULL cdf or output");
+  if (T < 1 || T > kMaxT) return fail(IBL_EINVAL, "T must lie in [1, 64]");
+  if (n < 0 || B < 0) return fail(IBL_EINVAL, "negative shape");
+  if (ld < B) return fail(IBL_EINVAL, "ld must be >= B");
+  if (out_dtype != kU8 && out_dtype != kI32 && out_dtype != kF32 && out_dtype != kF64)
+    return fail(IBL_EINVAL, "unknown output dtype");
+  if ((out_dtype == kF32 || out_dtype == kF64) && !llr) return fail(IBL_EINVAL, "LLR output needs llr[T]");
+  if (out_dtype == kU8 && T > 256) return fail(IBL_EINVAL, "u8 output needs T <= 256");
+  ChArgs a{};
+  for (int w = 0; w <= T; ++w) a.cdf[w] = cdf[w];
+  if (llr)
+    for (int w = 0; w < T; ++w) a.llr[w] = llr[w];
+  a.ctr[0] = offset;
+  a.key[0] = seed;
+  a.bits = d_bits;
+  a.out = d_out;
+  a.total = (int64_t)n * B;
+  a.ld = ld;
+  a.B = B;
+  a.T = T;
+  a.dtype = out_dtype;
+  if (a.total == 0) return IBL_OK;
+  HIPCHK(launch_ch_sample(a, (hipStream_t)stream));
+  return IBL_OK;
+}
+
 int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
                     int64_t* d_count, void* stream) {
   if (!d_x || !d_count) return fail(IBL_EINVAL, "NULL buffer");

@@ -126,6 +126,20 @@ hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);
 hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s);
+// ------------------------------------------------------------ channel generation
+constexpr int kMaxT = 64;         // largest channel alphabet of ibl_channel_sample
+struct ChArgs {
+  double cdf[kMaxT + 1];    // p(t | x = 0) CDF, cdf[0] = 0
+  double llr[kMaxT];        // output_LLRs (LLR outputs)
+  uint64_t ctr[4];          // Philox counter before the batch (numpy Philox `counter`)
+  uint64_t key[2];          // Philox key (numpy Philox `key`)
+  const uint8_t* bits;      // optional [n][B] codeword bits (1 mirrors the cluster), nullptr = all-zero
+  void* out;                // [n][ld] u8 / i32 cluster ids or f32 / f64 LLRs
+  int64_t total, ld;        // n*B, output row stride (elements)
+  int32_t B, T, dtype;
+};
+hipError_t launch_ch_sample(const ChArgs& a, hipStream_t s);
+
 hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
                               unsigned long long* cnt, hipStream_t s);
 

@@ -188,3 +188,42 @@ def count_below(x: torch.Tensor, rows: int, threshold: float, out: Optional[torc
                                            float(threshold), out.data_ptr(), _stream_ptr(x.device)),
                "ibl_count_below")
     return out
+
+
+def philox_blocks(n: int, B: int) -> int:
+    """Philox counter blocks one channel batch of n*B values consumes (4 values per block)."""
+    return (int(n) * int(B) + 3) // 4
+
+
+def channel_sample(out: torch.Tensor, cdf: np.ndarray, seed: int, offset: int,
+                   llr: Optional[np.ndarray] = None, bits: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Direct-inversion channel samples on the device (``ibl_channel_sample``; the reference's
+    ``quantize_direct_OpenCL`` / ``quantize_direct_OpenCL_LLR``, AWGN_Quantizer_BPSK.py:216-260).
+
+    ``out``: contiguous [n][B] device tensor — uint8 / int32 receive cluster ids, float32 / float64
+    receive ``llr[cluster]``. ``cdf``: the quantiser's T+1 CDF of p(t | x = 0). Uniforms come from
+    numpy-compatible Philox4x64-10 (counter ``offset``, key ``seed``); the batch consumes
+    :func:`philox_blocks` counter blocks. ``bits`` (optional [n][B] uint8 device tensor): codeword
+    bits, 1 mirrors the cluster."""
+    if out.dim() != 2 or not out.is_contiguous() or out.device.type != "cuda":
+        raise ValueError("out must be a contiguous 2-D device tensor")
+    if out.dtype not in _DT_ANY:
+        raise ValueError("out dtype must be uint8, int32, float32 or float64")
+    cdf = np.ascontiguousarray(cdf, dtype=np.float64)
+    T = len(cdf) - 1
+    llr_arr = None
+    if out.dtype in _DT_FL:
+        if llr is None or len(llr) != T:
+            raise ValueError("LLR output needs llr with T entries")
+        llr_arr = np.ascontiguousarray(llr, dtype=np.float64)
+    n, B = out.shape
+    bptr = None
+    if bits is not None:
+        if bits.dtype != torch.uint8 or bits.shape != out.shape or not bits.is_contiguous() or bits.device != out.device:
+            raise ValueError("bits must be a contiguous uint8 tensor shaped like out, on the same device")
+        bptr = bits.data_ptr()
+    _lib.check(_lib.load().ibl_channel_sample(cdf, T, None if llr_arr is None else llr_arr.ctypes.data,
+                                              int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), n, B, bptr,
+                                              out.data_ptr(), _DT_ANY[out.dtype], B, _stream_ptr(out.device)),
+               "ibl_channel_sample")
+    return out

@@ -32,9 +32,9 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(_HERE, "ib_oracle.c")
-        if not os.path.exists(_LIB_PATH) or (
-                os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_LIB_PATH)):
+        srcs = [os.path.join(_HERE, f) for f in ("ib_oracle.c", "channel_oracle.c")]
+        if not os.path.exists(_LIB_PATH) or any(
+                os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_LIB_PATH) for src in srcs):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         i32, i64 = ctypes.c_int32, ctypes.c_int64
@@ -52,6 +52,11 @@ def lib():
             getattr(L, nm).argtypes = [_f64p, i32]
         L.ibo_boxplus.restype = ctypes.c_double
         L.ibo_boxplus.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_double]
+        _u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+        _u8p = ctypes.c_void_p
+        L.ibo_philox_raw.argtypes = [_u64p, _u64p, i64, _u64p]
+        L.ibo_invert_cdf.argtypes = [_f64p, i64, _f64p, i32, _u8p, _i32p]
+        L.ibo_channel_sample.argtypes = [_f64p, i32, ctypes.c_uint64, ctypes.c_uint64, i64, _u8p, _i32p]
         _lib = L
     return _lib
 
@@ -118,3 +123,36 @@ def vn_sum(m) -> float:
 
 def boxplus(a: float, b: float, llr_max: float = 150.0) -> float:
     return float(lib().ibo_boxplus(a, b, llr_max))
+
+
+# ---------------------------------------------------------------- channel generation
+def philox_raw(counter: int, key: int, count: int) -> np.ndarray:
+    """First `count` 64-bit outputs of Philox4x64-10 in numpy's stream layout
+    (np.random.Philox(counter=counter, key=key).random_raw(count))."""
+    ctr = np.array([(counter >> (64 * i)) & (2 ** 64 - 1) for i in range(4)], dtype=np.uint64)
+    k = np.array([(key >> (64 * i)) & (2 ** 64 - 1) for i in range(2)], dtype=np.uint64)
+    out = np.zeros(count, np.uint64)
+    lib().ibo_philox_raw(ctr, k, count, out)
+    return out
+
+
+def invert_cdf(u: np.ndarray, cdf: np.ndarray, bits: np.ndarray | None = None) -> np.ndarray:
+    """Reference direct-inversion rule (kernels_quanti_template.cl:19-28; bit 1 mirrors,
+    AWGN_Quantizer_BPSK.py:137-143): t = #{w in 1..T: u > cdf[w]} (t = T clamped to T-1)."""
+    u = _c(u, np.float64)
+    cdf = _c(cdf, np.float64)
+    out = np.zeros(u.shape, np.int32)
+    b = None if bits is None else np.ascontiguousarray(bits, dtype=np.uint8)
+    lib().ibo_invert_cdf(u.ravel(), u.size, cdf, len(cdf) - 1, None if b is None else b.ctypes.data,
+                         out.reshape(-1))
+    return out
+
+
+def channel_sample(cdf: np.ndarray, seed: int, offset: int, n: int, B: int,
+                   bits: np.ndarray | None = None) -> np.ndarray:
+    """ibl_channel_sample restated: [n][B] int32 cluster ids."""
+    cdf = _c(cdf, np.float64)
+    out = np.zeros((n, B), np.int32)
+    b = None if bits is None else np.ascontiguousarray(bits, dtype=np.uint8)
+    lib().ibo_channel_sample(cdf, len(cdf) - 1, seed, offset, n * B, None if b is None else b.ctypes.data, out)
+    return out

@@ -1,0 +1,196 @@
+"""CPU: channel generation oracle (Philox stream vs numpy, inversion rule vs the reference's
+quantize_direct golden vectors), the drop-in quantiser's host paths, decoder-config I/O and the
+BER driver's Eb/N0 state machine (scripted decoder; gloo world size 2 for the counter reduction)."""
+import os
+import pickle
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from informationbottleneckdecodingldpc_amd import tables, tables_io
+from informationbottleneckdecodingldpc_amd.awgn_quantizer import AWGN_Channel_Quantizer
+from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
+from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+from oracle import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_channel.npz")
+
+
+@pytest.mark.parametrize("counter,key,count", [(0, 0, 13), (12345, 987654321, 64), (2 ** 64 - 3, 5, 40),
+                                               (7, 2 ** 64 - 1, 9), (2 ** 70 + 1, 3, 8)])
+def test_philox_stream_equals_numpy(counter, key, count):
+    ref = np.random.Philox(counter=counter, key=key).random_raw(count)
+    assert np.array_equal(oracle.philox_raw(counter, key, count), ref)
+
+
+@pytest.mark.parametrize("seed,offset,n,B", [(0, 0, 5, 7), (42, 1000, 3, 1), (2 ** 40 + 7, 2 ** 64 - 2, 4, 6)])
+def test_channel_sample_layout_is_numpy_random(seed, offset, n, B):
+    q = UniformQuantizer(sigma2_from_ebn0(0.6, 0.5))
+    u = np.random.Generator(np.random.Philox(counter=offset, key=seed)).random(n * B).reshape(n, B)
+    want = oracle.invert_cdf(u, q.cdf_t_given_x_equals_zero)
+    assert np.array_equal(oracle.channel_sample(q.cdf_t_given_x_equals_zero, seed, offset, n, B), want)
+
+
+def test_batches_continue_the_stream():
+    q = UniformQuantizer(sigma2_from_ebn0(1.0, 0.5))
+    cdf = q.cdf_t_given_x_equals_zero
+    full = oracle.channel_sample(cdf, 9, 100, 8, 16)
+    a = oracle.channel_sample(cdf, 9, 100, 4, 16)
+    b = oracle.channel_sample(cdf, 9, 100 + (4 * 16 + 3) // 4, 4, 16)
+    assert np.array_equal(np.vstack([a, b]), full)
+
+
+def _golden_cases():
+    z = np.load(GOLD, allow_pickle=False)
+    for k in range(int(z["ncases"])):
+        for kind in ("zero", "bits"):
+            p = f"c{k}_{kind}_"
+            yield (k, kind, int(z[p + "T"]), int(z[p + "seed"]), z[p + "cdf"], z[p + "bits"], z[p + "t"])
+
+
+@pytest.mark.parametrize("case", list(_golden_cases()), ids=lambda c: f"c{c[0]}-{c[1]}")
+def test_inversion_rule_equals_reference_quantize_direct(case):
+    _, _, T, seed, cdf, bits, t_ref = case
+    n, B = bits.shape
+    u = np.random.RandomState(seed).rand(n, B)
+    got = oracle.invert_cdf(u, cdf, bits)
+    assert np.array_equal(got.reshape(t_ref.shape) if B > 1 else got[:, 0], t_ref)
+    assert got.min() >= 0 and got.max() < T
+
+
+@pytest.mark.parametrize("case", list(_golden_cases()), ids=lambda c: f"c{c[0]}-{c[1]}")
+def test_dropin_host_quantize_direct_equals_reference(case):
+    _, _, T, seed, cdf, bits, t_ref = case
+    q = AWGN_Channel_Quantizer.from_generated(cdf)
+    np.random.seed(seed)
+    assert np.array_equal(q.quantize_direct(bits), t_ref)
+
+
+def test_dropin_quantizer_host_contract():
+    q = AWGN_Channel_Quantizer(sigma2_from_ebn0(0.6, 0.5), 3, 16, 2000)
+    assert q.cdf_t_given_x_equals_zero.shape == (17,) and q.output_LLRs.shape == (16,)
+    assert np.all(np.diff(q.output_LLRs) > 0)                      # clusters ordered by LLR
+    assert np.all(q.output_LLRs[:8] < 0) and np.all(q.output_LLRs[8:] > 0)
+    y = np.array([[-5.0, -2.9, -0.01, 0.01, 2.9, 5.0]]).T
+    assert list(q.quantize_on_host(y)) == [0, 0, 7, 8, 15, 15]
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        q.init_OpenCL_quanti(10, 4)
+
+
+# ---------------------------------------------------------------- decoder configuration I/O
+def _cfg():
+    tb = tables.random_tables(16, 16, 7, 8, 5, seed=2)
+    return tb, tables_io.config_from_tables(tb, EbN0=0.6)
+
+
+@pytest.mark.parametrize("ext", [".npz", ".json", ".pkl"])
+def test_decoder_config_roundtrip(tmp_path, ext):
+    tb, cfg = _cfg()
+    p = str(tmp_path / f"decoder_config{ext}")
+    if ext == ".pkl":
+        with open(p, "wb") as fh:                        # as the reference's save_config writes it
+            pickle.dump(dict(cfg), fh, protocol=-1)
+    else:
+        tables_io.save_decoder_config(p, cfg)
+    got = tables_io.load_decoder_config(p)
+    for k in tables_io.REFERENCE_KEYS:
+        assert np.array_equal(np.asarray(got[k]), np.asarray(cfg[k])), k
+    tb2 = tables_io.tables_from_config(got, 7, 8)
+    assert np.array_equal(tb2.cn, tb.cn) and np.array_equal(tb2.match_vn, tb.match_vn) and tb2.imax == 5
+
+
+class _Evil:
+    def __reduce__(self):
+        return (os.system, ("echo pwned",))
+
+
+def test_pickle_loader_refuses_code(tmp_path):
+    p = str(tmp_path / "evil.pkl")
+    with open(p, "wb") as fh:
+        pickle.dump({"imax": 3, "x": _Evil()}, fh)
+    with pytest.raises(pickle.UnpicklingError, match="refused global"):
+        tables_io.load_decoder_config(p)
+
+
+# ------------------------------------------------------------------------ BER driver (CPU)
+class _FakeQuanti:
+    def __init__(self, s2):
+        self.sigma_n2, self.seed, self.offset, self.context = s2, 0, 0, "cpu"
+
+    def init_OpenCL_quanti(self, N, B, return_buffer_only=False, context_=None):
+        self.B = B
+
+    def quantize_direct_OpenCL(self, N, B, dtype=None):
+        self.offset += 1
+        return self.sigma_n2
+
+
+class _FakeIB:
+    """Errors per block fall 10x per dB: BER(EbN0) = 10^(-2 - 10*EbN0)... scripted via sigma."""
+    codeword_len, R_c = 1000, 0.5
+
+    def __init__(self, rate_of):
+        self.rate_of, self.device = rate_of, None
+
+    def init_OpenCL_decoding(self, msg_at_time, ctx):
+        self.B = msg_at_time
+
+    def decode_OpenCL(self, rec, buffer_in=False, return_buffer=False):
+        return rec
+
+    def return_errors_all_zero(self, s2):
+        return self.rate_of(s2) * self.B
+
+
+def test_ber_state_machine_steps_and_stops():
+    # errors per codeword as a function of sigma^2 -> BER = e / (R_c * N)
+    def rate(s2):
+        ebn0 = -10 * np.log10(s2 * 2 * 0.5)
+        return 500 * 10 ** (-4 * ebn0)          # BER 1 at 0 dB, 1e-4 at 1 dB ...
+    cfg = BERConfig(EbN0_dB_start=0.0, EbN0_dB_max_value=2.0, target_error_rate=1e-7,
+                    BER_go_on_in_smaller_steps=5e-4, EbN0_dB_normal_stepwidth=0.25, EbN0_dB_small_stepwidth=0.5,
+                    min_errors=100, msg_at_time=10, max_blocks=10_000)
+    r = run_ber(_FakeIB(rate), cfg, quantizer_factory=_FakeQuanti)
+    assert np.allclose(r.EbN0_dB_vector, [0.0, 0.25, 0.5, 0.75, 1.0, 1.5, 2.0])
+    assert np.allclose(r.BER_vector[:3], [1.0, 10 ** -1, 10 ** -2], rtol=1e-9)
+    assert r.blocks[0] == 10 and r.errors[0] >= 100
+    assert r.blocks[-1] == 10_000                 # bounded by max_blocks
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ber_worker(rank, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        # rank 1 sees twice the errors: the summed counter must drive both ranks identically
+        cfg = BERConfig(EbN0_dB_start=0.0, EbN0_dB_max_value=0.0, min_errors=90, msg_at_time=10, sync_every=2)
+        r = run_ber(_FakeIB(lambda s2: 1.0 * (rank + 1)), cfg, quantizer_factory=_FakeQuanti)
+        q.put((rank, list(r.errors), list(r.blocks)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ber_counters_reduce_over_gloo_ranks():
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_ber_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, e0, b0), (r1, e1, b1) = res
+    # per sync (2 batches per rank): 2*10*1 + 2*10*2 = 60 errors, 40 blocks -> stops after 2 syncs
+    assert e0 == e1 == [120] and b0 == b1 == [80]
