@@ -155,7 +155,7 @@ struct ibl_ib {
   int32_t *flags = nullptr, *dL = nullptr;
   // fast path
   uint32_t *cn_img = nullptr, *vn_img = nullptr, *dec_img = nullptr;
-  int cn_nt = 0, vn_nt = 0, dec_nt = 0;
+  int cn_nt = 0, vn_nt = 0, dec_nt = 0;   // fast path: LDS table regions (4 tables each) per pass
   int32_t cn_fslot[kMaxD + 1] = {0}, vn_fslot[kMaxD + 1] = {0};
   KCfg kcn, kvn, kdec;
   KTimer timer;
@@ -294,10 +294,18 @@ Table make_table(int T, const std::function<int(int, int)>& f) {
   return tb;
 }
 
-void append(std::vector<uint32_t>& img, const Table& tb) {
-  for (int r = 0; r < 64; ++r)
-    img.push_back((uint32_t)tb[4 * r] | ((uint32_t)tb[4 * r + 1] << 8) | ((uint32_t)tb[4 * r + 2] << 16) |
-                  ((uint32_t)tb[4 * r + 3] << 24));
+// One pass's tables as 32-KiB LDS regions (kRegion): nreg x 256 dwords, dword (t*16+m) of region R
+// holds entry (t, m) of table 4R+j in byte j (slot_off). Unused slots of the last region are 0.
+void append_pass(std::vector<uint32_t>& img, const std::vector<Table>& tbs, int nreg) {
+  for (int R = 0; R < nreg; ++R)
+    for (int r = 0; r < 256; ++r) {
+      uint32_t w = 0;
+      for (int j = 0; j < 4; ++j) {
+        const size_t k = (size_t)4 * R + j;
+        if (k < tbs.size()) w |= (uint32_t)tbs[k][r] << (8 * j);
+      }
+      img.push_back(w);
+    }
 }
 
 std::vector<int> present(const std::vector<int32_t>& deg) {
@@ -308,7 +316,7 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
 }
 
 int pick_cfg(int which, int maxd, int nt, int num_cus, KCfg* k) {
-  k->lds = (size_t)nt * kTbl;
+  k->lds = (size_t)regions_of(nt) * kRegion;
   int best_waves = 0;
   for (int block : {512, 768, 1024, 384, 640, 256}) {
     int bpc = 0;
@@ -379,7 +387,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     cn_nt += (int)cdeg.size();
     for (int d : vdeg) vn_nt += (d >= 2);
   }
-  const int max_nt = kLdsBytes / kTbl;
+  const int max_nt = (kLdsBytes / kRegion) * 4;
   h->fast = !(flags & IBL_FLAG_FORCE_GENERIC) && Tc == T && T <= kTP && deg_ok && cn_nt <= max_nt &&
             vn_nt <= max_nt && VM <= max_nt && cn_nt > 0;
 
@@ -394,7 +402,8 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       return cn_lut[idx];
     };
     for (int p = 0; p < imax; ++p) {
-      for (int l = 0; l < cn_nraw; ++l) append(cimg, make_table(T, [&](int t, int m) { return cn_raw(p, l, t, m); }));
+      std::vector<Table> tbs;
+      for (int l = 0; l < cn_nraw; ++l) tbs.push_back(make_table(T, [&](int t, int m) { return cn_raw(p, l, t, m); }));
       int slot = cn_nraw;
       for (int d : cdeg) {
         if (!h->match) {
@@ -402,12 +411,13 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
           continue;
         }
         const int64_t mrow = (int64_t)p * T * CM + (int64_t)(d - 1) * T;
-        if (d == 2) append(cimg, make_table(T, [&](int t, int) { return match_cn[mrow + t]; }));
-        else append(cimg, make_table(T, [&](int t, int m) { return match_cn[mrow + cn_raw(p, d - 3, t, m)]; }));
+        if (d == 2) tbs.push_back(make_table(T, [&](int t, int) { return match_cn[mrow + t]; }));
+        else tbs.push_back(make_table(T, [&](int t, int m) { return match_cn[mrow + cn_raw(p, d - 3, t, m)]; }));
         h->cn_fslot[d] = slot++;
       }
+      append_pass(cimg, tbs, regions_of(cn_nt));
     }
-    h->cn_nt = cn_nt;
+    h->cn_nt = regions_of(cn_nt);
     // ---------------- VN images: pass k = 0 .. imax-2 (extrinsic), decision images k = 0 .. imax-1
     auto vn_raw = [&](int k, int l, int t, int m) -> int {
       const int64_t off = (int64_t)k * ((int64_t)Tc * T + (int64_t)(VM - 1) * T2);
@@ -415,7 +425,8 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       return vn_lut[idx];
     };
     for (int k = 0; k < std::max(imax - 1, 1); ++k) {
-      for (int l = 0; l < vn_nraw; ++l) append(vimg, make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
+      std::vector<Table> tbs;
+      for (int l = 0; l < vn_nraw; ++l) tbs.push_back(make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
       int slot = vn_nraw;
       for (int d : vdeg) {
         if (d < 2) continue;
@@ -424,19 +435,23 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
           continue;
         }
         const int64_t mrow = (int64_t)k * T * VM + (int64_t)(d - 1) * T;
-        append(vimg, make_table(T, [&](int t, int m) { return match_vn[mrow + vn_raw(k, d - 2, t, m)]; }));
+        tbs.push_back(make_table(T, [&](int t, int m) { return match_vn[mrow + vn_raw(k, d - 2, t, m)]; }));
         h->vn_fslot[d] = slot++;
       }
+      append_pass(vimg, tbs, regions_of(std::max(vn_nt, 1)));
     }
-    h->vn_nt = vn_nt;
-    for (int k = 0; k < imax; ++k)
-      for (int l = 0; l < VM; ++l) append(dimg, make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
-    h->dec_nt = VM;
+    h->vn_nt = regions_of(std::max(vn_nt, 1));
+    for (int k = 0; k < imax; ++k) {
+      std::vector<Table> tbs;
+      for (int l = 0; l < VM; ++l) tbs.push_back(make_table(T, [&](int t, int m) { return vn_raw(k, l, t, m); }));
+      append_pass(dimg, tbs, regions_of(VM));
+    }
+    h->dec_nt = regions_of(VM);
     if ((rc = dupload(&h->cn_img, cimg.data(), cimg.size())) || (rc = dupload(&h->vn_img, vimg.data(), vimg.size())) ||
         (rc = dupload(&h->dec_img, dimg.data(), dimg.size())))
       return bail(rc);
-    if ((rc = pick_cfg(0, CM, h->cn_nt, g->num_cus, &h->kcn)) || (rc = pick_cfg(1, VM, std::max(h->vn_nt, 1), g->num_cus, &h->kvn)) ||
-        (rc = pick_cfg(2, VM, h->dec_nt, g->num_cus, &h->kdec)))
+    if ((rc = pick_cfg(0, CM, 4 * h->cn_nt, g->num_cus, &h->kcn)) || (rc = pick_cfg(1, VM, 4 * h->vn_nt, g->num_cus, &h->kvn)) ||
+        (rc = pick_cfg(2, VM, 4 * h->dec_nt, g->num_cus, &h->kdec)))
       return bail(rc);
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
@@ -518,10 +533,10 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     cn.in = h->cin; cn.gather = nullptr;
     for (int j = 1; j < I; ++j) {
       const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-      vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 64;
+      vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
       vn.gate = gate;
       HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_fast(vn, h->VM, h->kvn.grid, h->kvn.block, h->kvn.lds, s); }));
-      cn.img = h->cn_img + (size_t)j * h->cn_nt * 64;
+      cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
       cn.gate = gate;
       cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
       HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));

@@ -22,7 +22,13 @@ constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, 
 constexpr int kW = IBL_W;
 constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
 constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item
-constexpr int kTbl = 8192;        // one IB lookup table replicated over the 32 LDS banks
+constexpr int kTbl = 8192;        // LDS bytes per IB lookup table (replicated over the 32 banks)
+// LDS table layout: 4 tables interleaved per 32-KiB region — byte (slot & 3) of the dword at row
+// t*16+m, bank lane&31 holds entry (t, m) of table `slot`, so a lookup address is
+// (t << 11) | (m << 7) | 4*(lane&31) + slot_off(slot) with the slot in the DS immediate.
+constexpr int kRegion = 4 * kTbl;
+__host__ __device__ constexpr uint32_t slot_off(int s) { return (uint32_t)(s >> 2) * kRegion + (uint32_t)(s & 3); }
+constexpr int regions_of(int nt) { return (nt + 3) >> 2; }
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
 constexpr int kMaxD = 16;
 constexpr int kLightD = 4;        // nodes up to this degree run with a 4-row item buffer         // largest node degree with an unrolled fast-path body
@@ -43,7 +49,7 @@ struct IbFastArgs {
   const int32_t* gate;      // kShards flag words that must be non-zero to run (nullptr: run)
   int32_t* unsat;           // kShards flag words to set when a check is unsatisfied (nullptr: no syndrome)
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
-  int32_t nt;               // tables staged in LDS
+  int32_t nt;               // 32-KiB table regions staged in LDS (4 tables each)
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
 };

@@ -44,14 +44,21 @@ __device__ __forceinline__ uint32_t lu(uint32_t x, uint32_t c) {
   asm("" : "+v"(x));
   return *(lds8_t*)(size_t)(x + c);
 }
+// chained lookup: table value t of the previous step, column term q. The row/column merge is one
+// v_lshl_or_b32 per lookup written out, so the compiler cannot hoist t << 11 into a shared
+// shift + separate ORs (3 ops for the 2 lookups that read each prefix value P_w).
+__device__ __forceinline__ uint32_t luc(uint32_t t, uint32_t q, uint32_t c) {
+  uint32_t x;
+  asm("v_lshl_or_b32 %0, %1, 11, %2" : "=v"(x) : "v"(t), "v"(q));
+  return *(lds8_t*)(size_t)(x + c);
+}
 __device__ __forceinline__ uint32_t lds_base(const uint8_t* p) { return (uint32_t)(size_t)(lds8_t*)p; }
 __device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
   if (lds_base(lds) != 0u) __builtin_trap();  // uniform scalar test; never taken without static LDS
 }
 
-__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
-  return ((m >> 2) << 7) + (m & 3u) + lane4;
-}
+// column term of a lookup: (m << 7) | 4*(lane & 31); the row term of t is t << 11 (see kRegion)
+__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) { return (m << 7) | lane4; }
 
 __device__ __forceinline__ uint32_t valid_mask4(int remaining) {
   return remaining >= 4 ? 0xFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
@@ -62,9 +69,10 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
   return __ballot(gate[lane] != 0) != 0ull;
 }
 
-__device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nt) {
+// img: nreg regions x 256 dwords (row t*16+m, byte j = table 4R+j); replicated over the 32 banks
+__device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nreg) {
   uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
-  const int n = nt * (kTbl / 4);
+  const int n = nreg * (kRegion / 4);
   for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
 }
 
@@ -197,7 +205,7 @@ __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D],
                                         uint32_t (&outw)[D]) {
   // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
   auto sb = [&](int j, int l) -> uint32_t {
-    return j == D - 1 ? 0u : (l == D - 3) ? fbase : (uint32_t)(l * kTbl);
+    return j == D - 1 ? 0u : (l == D - 3) ? fbase : slot_off(l);
   };
 #if IBL_CN_UNROLL
 #pragma unroll
@@ -218,7 +226,7 @@ __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D],
 #pragma unroll
     for (int j = 2; j < D; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 2));
+      for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 2));
     outw[0] |= pack4n(t, g);
 #pragma unroll
     for (int s = 0; s < 4; ++s) P[s] = nib(in[0], 4 * g + s);
@@ -229,10 +237,10 @@ __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D],
 #pragma unroll
       for (int j = w + 1; j < D; ++j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 2));
+        for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 2));
       outw[w] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) P[s] = lu((P[s] << 9) + q[w][s], sb(w, w - 1));
+      for (int s = 0; s < 4; ++s) P[s] = luc(P[s], q[w][s], sb(w, w - 1));
     }
     outw[D - 1] |= pack4n(P, g);
   }
@@ -249,7 +257,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 #pragma unroll
     for (int i = 0; i < W; ++i) outw[w][i] = 0;
   }
-  const uint32_t fbase = (uint32_t)fslot * kTbl;
+  const uint32_t fbase = slot_off(fslot);
   if (do_par) {
 #pragma unroll
     for (int i = 0; i < W; ++i) {
@@ -279,8 +287,8 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
           uint32_t t0[4], t1[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            t0[s] = lu((nib(in[1], 4 * g + s) << 9) + lane4, fbase);
-            t1[s] = lu((nib(in[0], 4 * g + s) << 9) + lane4, fbase);
+            t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
+            t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
           }
           o[0] |= pack4n(t0, g);
           o[1] |= pack4n(t1, g);
@@ -309,7 +317,7 @@ __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D],
                                         uint32_t fbase, uint32_t (&outw)[D]) {
   // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
   auto sb = [&](int j, int l) -> uint32_t {
-    return j == D - 1 ? 0u : (l == D - 2) ? fbase : (uint32_t)(l * kTbl);
+    return j == D - 1 ? 0u : (l == D - 2) ? fbase : slot_off(l);
   };
 #if IBL_VN_UNROLL
 #pragma unroll
@@ -325,13 +333,13 @@ __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D],
 #pragma unroll
     for (int s = 0; s < 4; ++s) q[D - 1][s] += fbase;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) c[s] = nib(chw, 4 * g + s) << 9;
+    for (int s = 0; s < 4; ++s) c[s] = nib(chw, 4 * g + s) << 11;
 #pragma unroll
     for (int s = 0; s < 4; ++s) t[s] = lu(c[s] + q[1][s], sb(1, 0));
 #pragma unroll
     for (int j = 2; j < D; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 1));
+      for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 1));
     outw[0] |= pack4n(t, g);
 #pragma unroll
     for (int s = 0; s < 4; ++s) Q[s] = lu(c[s] + q[0][s], sb(0, 0));
@@ -342,10 +350,10 @@ __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D],
 #pragma unroll
       for (int j = w + 1; j < D; ++j)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = lu((t[s] << 9) + q[j][s], sb(j, j - 1));
+        for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 1));
       outw[w] |= pack4n(t, g);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) Q[s] = lu((Q[s] << 9) + q[w][s], sb(w, w));
+      for (int s = 0; s < 4; ++s) Q[s] = luc(Q[s], q[w][s], sb(w, w));
     }
     outw[D - 1] |= pack4n(Q, g);
   }
@@ -357,7 +365,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, 
   uint32_t outw[D][W], trow[D];
 #pragma unroll
   for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
-  const uint32_t fbase = (uint32_t)fslot * kTbl;
+  const uint32_t fbase = slot_off(fslot);
 #pragma unroll
   for (int i = 0; i < W; ++i) {
     if constexpr (D == 1) {
@@ -418,9 +426,9 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int k = 4 * g + s;
-      uint32_t Q = lu((nib(cw, k) << 9) + qidx(nib(inw[0], k), lane4), 0);
+      uint32_t Q = lu((nib(cw, k) << 11) + qidx(nib(inw[0], k), lane4), 0);
 #pragma unroll
-      for (int l = 1; l < D; ++l) Q = lu((Q << 9) + qidx(nib(inw[l], k), lane4), l * kTbl);
+      for (int l = 1; l < D; ++l) Q = luc(Q, qidx(nib(inw[l], k), lane4), slot_off(l));
       packed |= Q << (8 * s);
     }
     store4(a.out, a.out_dtype, (size_t)node * a.B, cwb + 4 * g, a.B, a.aligned != 0, packed);
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
   const int lane = threadIdx.x & 63;
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
   lds_at_zero(lds);
-  stage_tables(lds, a.img + (size_t)L * a.nt * 64, a.nt);
+  stage_tables(lds, a.img + (size_t)L * a.nt * 256, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
   const int wpb = blockDim.x >> 6;
