@@ -30,7 +30,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB
     variant objects go to build/<tag>/."""
     objdir = os.path.join(PKG, "build", tag) if tag else os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
-    headers = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "ibldpc.h")]
+    headers = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "ibldpc.h")] + \
+        [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".inc")]
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)

@@ -185,65 +185,23 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
   return (t[0] | (t[1] << 4) | (t[2] << 8) | (t[3] << 12)) << (16 * g);
 }
 
-// Group loop (two groups of 4 codewords per dword): rolled keeps VGPRs low (more waves), unrolled
-// gives 8 independent chains per step.
-#ifndef IBL_CN_UNROLL
-#define IBL_CN_UNROLL 0
-#endif
-#ifndef IBL_VN_UNROLL
-#define IBL_VN_UNROLL 0
-#endif
-
 // ------------------------------------------------------------------ check node
 // Inputs in_0..in_{D-1} (CN order = ascending column). Output w is the left fold over the
 // other inputs with table l at fold step l (kernels_template_irreg.cl:226-231):
 //   out[0]   = fold(in_1, in_2, ...),   out[w] = fold(P_w, in_{w+1}, ...),  P_w = fold(in_0..in_{w-1})
 // Step l uses LDS slot l, except the last step (l = D-3) which uses fslot (matching composed).
-// One dword of each row = 8 codewords, run as two groups of 4 (4 independent reads per step).
+// The chains of one group of cn_sched_s(D) codewords run concurrently per the generated schedule
+// (tools/gen_sched.py -> ib_sched.inc: list scheduling of the fold DAG onto L chain lanes).
+#ifndef IBL_SCHED_FILE
+#define IBL_SCHED_FILE "ib_sched.inc"
+#endif
+#include IBL_SCHED_FILE
+
 template <int D>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         uint32_t (&outw)[D]) {
-  // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
-  auto sb = [&](int j, int l) -> uint32_t {
-    return j == D - 1 ? 0u : (l == D - 3) ? fbase : slot_off(l);
-  };
-#if IBL_CN_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
-  for (int g = 0; g < 2; ++g) {
-    uint32_t q[D][4];
-#pragma unroll
-    for (int j = 1; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) q[D - 1][s] += fbase;
-    uint32_t t[4], P[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = nib(in[1], 4 * g + s);
-#pragma unroll
-    for (int j = 2; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 2));
-    outw[0] |= pack4n(t, g);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) P[s] = nib(in[0], 4 * g + s);
-#pragma unroll
-    for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = P[s];
-#pragma unroll
-      for (int j = w + 1; j < D; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 2));
-      outw[w] |= pack4n(t, g);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) P[s] = luc(P[s], q[w][s], sb(w, w - 1));
-    }
-    outw[D - 1] |= pack4n(P, g);
-  }
+  for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, outw, k0);
 }
 
 template <int D, class Buf>
@@ -311,52 +269,12 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 // Inputs: channel c and in_0..in_{D-1} (VN order = ascending row). Extrinsic output w folds
 // c and the other inputs (kernels_template_irreg.cl:151-160): step 0 = channel table V_0,
 // step l = V_l; the last step (l = D-2) uses fslot (matching composed). Degree 1 forwards c
-// (:131-136).
+// (:131-136). Schedules as for the check node (vn_group in ib_sched.inc).
 template <int D>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, uint32_t (&outw)[D]) {
-  // q[D-1] only ever meets the final (composite) table: its base fbase is folded into q[D-1] once
-  auto sb = [&](int j, int l) -> uint32_t {
-    return j == D - 1 ? 0u : (l == D - 2) ? fbase : slot_off(l);
-  };
-#if IBL_VN_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
-  for (int g = 0; g < 2; ++g) {
-    uint32_t q[D][4], c[4], t[4], Q[4];
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) q[j][s] = qidx(nib(in[j], 4 * g + s), lane4);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) q[D - 1][s] += fbase;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) c[s] = nib(chw, 4 * g + s) << 11;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = lu(c[s] + q[1][s], sb(1, 0));
-#pragma unroll
-    for (int j = 2; j < D; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 1));
-    outw[0] |= pack4n(t, g);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) Q[s] = lu(c[s] + q[0][s], sb(0, 0));
-#pragma unroll
-    for (int w = 1; w <= D - 2; ++w) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) t[s] = Q[s];
-#pragma unroll
-      for (int j = w + 1; j < D; ++j)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) t[s] = luc(t[s], q[j][s], sb(j, j - 1));
-      outw[w] |= pack4n(t, g);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) Q[s] = luc(Q[s], q[w][s], sb(w, w));
-    }
-    outw[D - 1] |= pack4n(Q, g);
-  }
+  for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, outw, k0);
 }
 
 template <int D, class Buf>
@@ -509,8 +427,12 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #ifndef IBL_LB8
 #define IBL_LB8 1024
 #endif
+// minimum waves per SIMD for the MAXD=8 bodies (register budget 512 / waves); 1 = no constraint
+#ifndef IBL_WPE8
+#define IBL_WPE8 1
+#endif
 template <int MAXD, bool GATHER>
-__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512) void ib_cn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
@@ -520,7 +442,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512) void ib_cn_fast(IbFastAr
 }
 
 template <int MAXD>
-__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512) void ib_vn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1) void ib_vn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
   lds_at_zero(lds);

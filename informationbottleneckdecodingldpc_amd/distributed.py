@@ -35,6 +35,12 @@ def init_from_env(backend: str | None = None) -> Tuple[int, int, torch.device]:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not for production runs): IBL_SHARE_DEVICE=1 maps ranks onto the visible
+    # devices round-robin (several ranks on one GPU), IBL_DIST_BACKEND overrides the backend
+    # (RCCL needs one GPU per rank, so shared-device rehearsals use gloo)
+    if os.environ.get("IBL_SHARE_DEVICE") == "1" and torch.cuda.device_count() > 0:
+        local = local % torch.cuda.device_count()
+    backend = backend or os.environ.get("IBL_DIST_BACKEND") or None
     use_gpu = torch.cuda.is_available()
     device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:

@@ -1,0 +1,176 @@
+"""Generate the IB fast path's per-degree fold schedules (csrc/ib_sched.inc).
+
+The check-node (variable-node) update of one group of S codewords is a DAG of lookup chains
+(kernels_template_irreg.cl:205-231 / :151-160, prefix-shared as in ib_kernels.hip):
+  CN degree D:  out0 chain  in1 -> B0(.,in2) -> ... -> B_{D-3}(.,in_{D-1})           (D-2 steps)
+                P chain     in0 -> B0(.,in1) = P2 -> B1(.,in2) = P3 ... -> out_{D-1}  (D-2 steps)
+                chain w     P_w -> B_{w-1}(.,in_{w+1}) -> ... -> out_w, w=1..D-2     (D-1-w steps)
+  VN degree D:  out0 chain  V0(c,in1) -> V1(.,in2) -> ... -> out0                    (D-1 steps)
+                Q chain     V0(c,in0) = Q1 -> V1(.,in1) = Q2 ... -> out_{D-1}        (D-1 steps)
+                chain w     Q_w -> V_w(.,in_{w+1}) -> ... -> out_w, w=1..D-2         (D-1-w steps)
+Every chain is a sequence of dependent LDS lookups; chains are independent once their start value
+exists, so the critical path is D-2 (CN) / D-1 (VN) steps, not the 25 / 35 of running them one
+after another. This script list-schedules the chains onto L concurrent lanes (critical path first)
+and emits straight-line code with one SSA name per value (no register copies): each time step
+issues the lookups of every running lane for all S sub-slots back to back.
+
+usage: python tools/gen_sched.py [S_cn L_cn [S_vn L_vn]] > informationbottleneckdecodingldpc_amd/csrc/ib_sched.inc
+(measured on DVB-S2: CN S=4 L=2, VN S=2 L=4 — the default)
+"""
+import sys
+
+KMAXD = 16
+
+
+def slot_off(l):
+    return (l >> 2) * 32768 + (l & 3)
+
+
+def cn_chains(D):
+    def slot(j, l):
+        return "0u" if j == D - 1 else ("fbase" if l == D - 3 else f"{slot_off(l)}u")
+    ch = [dict(id="o0", start=("nib", 1), steps=[("q", j, slot(j, j - 2)) for j in range(2, D)], out=0),
+          dict(id="P", start=("nib", 0), steps=[("q", w, slot(w, w - 1)) for w in range(1, D - 1)], out=D - 1,
+               exports={i: f"P{i + 2}" for i in range(D - 2)})]     # after step i: P_{i+2}
+    for w in range(1, D - 1):
+        st = ("nib", 0) if w == 1 else ("val", "P", w - 2)          # P_w = P chain after step w-2
+        ch.append(dict(id=f"c{w}", start=st, steps=[("q", j, slot(j, j - 2)) for j in range(w + 1, D)], out=w))
+    return ch
+
+
+def vn_chains(D):
+    def slot(j, l):
+        return "0u" if j == D - 1 else ("fbase" if l == D - 2 else f"{slot_off(l)}u")
+    ch = [dict(id="o0", start=("chan",), steps=[("c", 1, slot(1, 0))] + [("q", j, slot(j, j - 1)) for j in range(2, D)],
+               out=0),
+          dict(id="Q", start=("chan",), steps=[("c", 0, slot(0, 0))] + [("q", w, slot(w, w)) for w in range(1, D - 1)],
+               out=D - 1)]
+    for w in range(1, D - 1):
+        ch.append(dict(id=f"c{w}", start=("val", "Q", w - 1),       # Q_w = Q chain after step w-1
+                       steps=[("q", j, slot(j, j - 1)) for j in range(w + 1, D)], out=w))
+    return ch
+
+
+def schedule(chains, L):
+    """List scheduling: returns [(time, [(chain, step_index), ...]), ...]."""
+    by_id = {c["id"]: c for c in chains}
+    # downstream weight: a prefix chain gates every suffix chain -> schedule it first
+    for c in chains:
+        c["prio"] = len(c["steps"]) + (100 if c["id"] in ("P", "Q") else 0)
+    ready_at = {}
+    for c in chains:
+        ready_at[c["id"]] = 0 if c["start"][0] in ("nib", "chan") else None
+    done_step = {}   # (chain, step) -> time
+    running = []     # [chain_id, next_step]
+    pending = [c["id"] for c in chains]
+    out = []
+    t = 0
+    while pending or running:
+        # fill lanes
+        cand = [cid for cid in pending if ready_at[cid] is not None and ready_at[cid] <= t]
+        cand.sort(key=lambda cid: (-by_id[cid]["prio"], chains.index(by_id[cid])))
+        while len(running) < L and cand:
+            cid = cand.pop(0)
+            pending.remove(cid)
+            running.append([cid, 0])
+        if not running:
+            raise RuntimeError("deadlock")
+        issued = []
+        for r in running:
+            issued.append((r[0], r[1]))
+            done_step[(r[0], r[1])] = t
+            r[1] += 1
+        out.append((t, issued))
+        # exports become available next step
+        for cid, k in issued:
+            for c in chains:
+                st = c["start"]
+                if st[0] == "val" and st[1] == cid and st[2] == k:
+                    ready_at[c["id"]] = t + 1
+        running = [r for r in running if r[1] < len(by_id[r[0]]["steps"])]
+        t += 1
+    return out
+
+
+def emit_body(kind, D, S, L):
+    chains = cn_chains(D) if kind == "cn" else vn_chains(D)
+    by_id = {c["id"]: c for c in chains}
+    sched = schedule(chains, L)
+    lines = []
+    qidx = sorted({st[1] for c in chains for st in c["steps"]})
+    for j in qidx:
+        for s in range(S):
+            extra = " + fbase" if j == D - 1 else ""
+            lines.append(f"  const uint32_t q{j}_{s} = qidx(nib(in[{j}], k0 + {s}), lane4){extra};")
+    if kind == "vn":
+        for s in range(S):
+            lines.append(f"  const uint32_t c_{s} = nib(chw, k0 + {s}) << 11;")
+
+    def name(cid, k, s):
+        return f"v_{cid}_{k}_{s}"
+
+    def start_val(c, s):
+        st = c["start"]
+        if st[0] == "nib":
+            return f"nib(in[{st[1]}], k0 + {s})"
+        if st[0] == "val":
+            return name(st[1], st[2], s)
+        raise AssertionError
+
+    for t, issued in sched:
+        lines.append(f"  // step {t}: " + ", ".join(f"{cid}[{k}]" for cid, k in issued))
+        for cid, k in issued:
+            c = by_id[cid]
+            op, j, sl = c["steps"][k]
+            for s in range(S):
+                if op == "c":
+                    expr = f"lu(c_{s} + q{j}_{s}, {sl})"
+                else:
+                    prev = start_val(c, s) if k == 0 else name(cid, k - 1, s)
+                    expr = f"luc({prev}, q{j}_{s}, {sl})"
+                lines.append(f"  const uint32_t {name(cid, k, s)} = {expr};")
+        for cid, k in issued:
+            c = by_id[cid]
+            if k == len(c["steps"]) - 1:
+                vals = [name(cid, k, s) for s in range(S)]
+                pk = vals[0]
+                for s in range(1, S):
+                    pk = f"{pk} | ({vals[s]} << {4 * s})"
+                lines.append(f"  o[{c['out']}] |= ({pk}) << (4 * k0);")
+    return lines
+
+
+def main():
+    """args: S_cn L_cn [S_vn L_vn] (group size and chain lanes per kernel, for degrees <= 8; larger
+    degrees use S = 2, L = 4 so the MAXD = 16 bodies keep their occupancy)."""
+    a = [int(x) for x in sys.argv[1:]] or [4, 2, 2, 4]
+    Sc, Lc = a[0], a[1]
+    Sv, Lv = (a[2], a[3]) if len(a) >= 4 else (Sc, Lc)
+
+    def cfg(S, L, D):
+        return (S, L) if D <= 8 else (2, 4)
+    print(f"// GENERATED by tools/gen_sched.py {' '.join(sys.argv[1:])} -- do not edit.")
+    print(f"// Fold schedules of the IB fast path (degrees <= 8): CN groups of {Sc} codewords with up to {Lc}")
+    print(f"// chains in flight, VN groups of {Sv} codewords with up to {Lv}; degrees > 8: 2 codewords, 4 chains.")
+    print(f"__host__ __device__ constexpr int cn_sched_s(int D) {{ return D <= 8 ? {Sc} : 2; }}")
+    print(f"__host__ __device__ constexpr int vn_sched_s(int D) {{ return D <= 8 ? {Sv} : 2; }}")
+    print("template <int D> __device__ __forceinline__ void cn_group(uint32_t lane4, const uint32_t (&in)[D],")
+    print("                                                         uint32_t fbase, uint32_t (&o)[D], int k0);")
+    print("template <int D> __device__ __forceinline__ void vn_group(uint32_t lane4, const uint32_t (&in)[D],")
+    print("                                                         uint32_t chw, uint32_t fbase, uint32_t (&o)[D],")
+    print("                                                         int k0);")
+    for D in range(3, KMAXD + 1):
+        print(f"template <> __device__ __forceinline__ void cn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
+        print(f"                                                         uint32_t fbase, uint32_t (&o)[{D}], int k0) {{")
+        print("\n".join(emit_body("cn", D, *cfg(Sc, Lc, D))))
+        print("}")
+    for D in range(2, KMAXD + 1):
+        print(f"template <> __device__ __forceinline__ void vn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
+        print(f"                                                         uint32_t chw, uint32_t fbase,")
+        print(f"                                                         uint32_t (&o)[{D}], int k0) {{")
+        print("\n".join(emit_body("vn", D, *cfg(Sv, Lv, D))))
+        print("}")
+
+
+if __name__ == "__main__":
+    main()

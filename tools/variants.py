@@ -13,6 +13,8 @@ VARIANTS = {
     "w2u": ["IBL_W=2", "IBL_CN_UNROLL=1", "IBL_LB8=512"],
     "w4": ["IBL_W=4", "IBL_LB8=512"],
     "w2b": ["IBL_W=2", "IBL_LB8=512"],
+    "wpe5": ["IBL_WPE8=5"],
+    "wpe6": ["IBL_WPE8=6"],
 }
 
 if __name__ == "__main__":
