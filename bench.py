@@ -218,6 +218,11 @@ def main():
                          "achieved_stored": round(achieved_stored, 1),
                          "frac_stored": round(achieved_stored / HBM_PEAK_GBPS, 4),
                          "lds_lookups_per_clk_per_cu": lds,
+                         "note": ("achieved/frac price SURVEY §8(d)'s u8 messages; this build stores 4-bit "
+                                  "messages, so the HBM bytes actually moved are achieved_stored/frac_stored "
+                                  "(a u8-equivalent frac above 1 is the nibble format beating the u8 roofline); "
+                                  "the kernel is bound by LDS lookups + VALU issue, see lds_lookups_per_clk_per_cu")
+                         if fmt == "u4" else None,
                          "launches": {"cn": cn_n, "vn": vn_n},
                          "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}},
             "cpu_baseline": cpu,

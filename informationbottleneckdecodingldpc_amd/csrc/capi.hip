@@ -9,6 +9,7 @@
 // are all zero, and a one-wave kernel turns the flags into the iteration index the output
 // pass uses.  The host only enqueues.
 #include <algorithm>
+#include <cstdio>
 #include <functional>
 #include <cstdlib>
 #include <cstring>
@@ -316,9 +317,10 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
 }
 
 int pick_cfg(int which, int maxd, int nt, int num_cus, KCfg* k) {
-  k->lds = (size_t)regions_of(nt) * kRegion;
+  k->lds = (size_t)regions_of(nt) * kRegion + 64;   // tables + the fast kernels' 2 work counters
   int best_waves = 0;
-  for (int block : {512, 768, 1024, 384, 640, 256}) {
+  // largest block first at equal occupancy: a CU's waves then share one work counter
+  for (int block : {1024, 768, 640, 512, 384, 256}) {
     int bpc = 0;
     if (ib_fast_occupancy(which, maxd, block, k->lds, &bpc) != hipSuccess) continue;
     const int waves = bpc * block / 64;
@@ -531,15 +533,36 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
     HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));
     cn.in = h->cin; cn.gather = nullptr;
+    // diagnostics: IBL_TRACE_WAVES=<prefix> records {start, end, items|cu} of every wave of the middle
+    // iteration's VN and CN launches into <prefix>_vn.bin / <prefix>_cn.bin (uint64 triples)
+    const char* trace_path = getenv("IBL_TRACE_WAVES");
+    uint64_t* trace = nullptr;
+    const size_t nwv = (size_t)h->kvn.grid * (h->kvn.block / 64), nwc = (size_t)h->kcn.grid * (h->kcn.block / 64);
+    if (trace_path && I > 1) HIPCHK(hipMalloc((void**)&trace, sizeof(uint64_t) * 3 * (nwv + nwc)));
     for (int j = 1; j < I; ++j) {
       const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
       vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
       vn.gate = gate;
+      vn.trace = (trace && j == I / 2) ? trace : nullptr;
       HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_fast(vn, h->VM, h->kvn.grid, h->kvn.block, h->kvn.lds, s); }));
       cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
       cn.gate = gate;
       cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
+      cn.trace = (trace && j == I / 2) ? trace + 3 * nwv : nullptr;
       HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));
+    }
+    if (trace) {
+      std::vector<uint64_t> hv(3 * (nwv + nwc));
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(hv.data(), trace, sizeof(uint64_t) * hv.size(), hipMemcpyDeviceToHost));
+      (void)hipFree(trace);
+      for (int k = 0; k < 2; ++k) {
+        const std::string p = std::string(trace_path) + (k == 0 ? "_vn.bin" : "_cn.bin");
+        if (FILE* f = fopen(p.c_str(), "wb")) {
+          fwrite(hv.data() + (k == 0 ? 0 : 3 * nwv), sizeof(uint64_t), 3 * (k == 0 ? nwv : nwc), f);
+          fclose(f);
+        }
+      }
     }
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     IbDecArgs dc{};

@@ -52,6 +52,7 @@ struct IbFastArgs {
   int32_t nt;               // 32-KiB table regions staged in LDS (4 tables each)
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
+  uint64_t* trace;          // diagnostics (IBL_TRACE_WAVES): per wave {start clock, end clock, items}, else nullptr
 };
 
 struct IbDecArgs {

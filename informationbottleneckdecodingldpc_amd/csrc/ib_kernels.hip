@@ -362,9 +362,16 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch). Positions are
 // heaviest-first: [0, n_heavy) run with a MAXD-row item buffer, the rest with a kLightD-row one
 // (a degree-2 node then issues 4 row loads, not MAXD).
+// one workgroup-wide ticket (lane 0 takes it, the wave reads it back as a scalar)
+__device__ __forceinline__ int take_ticket(int* ctr, int lane) {
+  int t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(t);
+}
+
 template <class Buf, bool VN, bool GATHER, int DLO>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, int lane, int first, int end, int nw,
-                                         bool do_par, bool& unsat) {
+                                         int wpb, int* ctr, bool do_par, bool& unsat, int& items_done) {
   // always inlined: an out-of-line body would take the item by reference through scratch
   auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
     settle(cur);
@@ -385,25 +392,40 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, in
       }
     }
   };
-  // ping-pong buffers (no register copies: a copy would wait for the prefetched loads). The
+  // Items of this phase: the block owns {first + b*wpb + w + nw*i} (the static round-robin share of
+  // its wpb waves), but hands them to its waves dynamically through a workgroup counter in LDS:
+  // waves on one SIMD issue oldest-first, so with equal static shares the youngest waves of every
+  // CU finished up to 1.5x later than the oldest (traced, IBL_TRACE_WAVES). Ticket k of the block
+  // maps to item first + b*wpb + (k % wpb) + nw*(k / wpb). A ticket is taken one item ahead, so
+  // the LDS atomic's latency overlaps the current item's lookups.
+  // Ping-pong buffers (no register copies: a copy would wait for the prefetched loads); the
   // prefetch is unconditional (clamped to the last item) so the control flow stays straight-line
   // and the compiler's wait for the current item leaves the next item's loads in flight.
+  const int base = first + (int)blockIdx.x * wpb;
+  auto item_of = [&](int k) { return base + (k % wpb) + nw * (k / wpb); };
   Buf A, Bb;
-  int item = first;
+  int item = item_of(take_ticket(ctr, lane));
   if (item >= end) return;
+  int done = 0;
   fetch_item<Buf, VN, GATHER>(a, item, lane, A);
+  int kn = take_ticket(ctr, lane);
   for (;;) {
-    int next = item + nw;
+    int next = item_of(kn);
     fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb);
+    kn = take_ticket(ctr, lane);
     compute(A);
+    ++done;
     if (next >= end) break;
     item = next;
-    next = item + nw;
+    next = item_of(kn);
     fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A);
+    kn = take_ticket(ctr, lane);
     compute(Bb);
+    ++done;
     if (next >= end) break;
     item = next;
   }
+  items_done += done;
 }
 
 template <int MAXD, bool VN, bool GATHER>
@@ -417,8 +439,17 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   const bool do_par = !VN && a.unsat != nullptr;
   bool unsat = false;
   constexpr int W = rowW<MAXD>();
-  ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane, gw, heavy_end, nw, do_par, unsat);
-  ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane, heavy_end + gw, nitems, nw, do_par, unsat);
+  const uint64_t t0 = a.trace ? __builtin_readcyclecounter() : 0;
+  int* ctr = reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + (size_t)a.nt * kRegion);  // 2 phase counters
+  int mine = 0;
+  ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat, mine);
+  ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par, unsat, mine);
+  if (a.trace && lane == 0) {
+    const uint64_t t1 = __builtin_readcyclecounter();
+    a.trace[3 * gw] = t0;
+    a.trace[3 * gw + 1] = t1;
+    a.trace[3 * gw + 2] = (uint64_t)mine | ((uint64_t)__smid() << 32);
+  }
   if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
 }
 
@@ -436,6 +467,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
+  if (threadIdx.x < 2) reinterpret_cast<int*>(lds + (size_t)a.nt * kRegion)[threadIdx.x] = 0;
   stage_tables(lds, a.img, a.nt);
   __syncthreads();
   ib_pass<MAXD, false, GATHER>(a, lds);
@@ -446,6 +478,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
   lds_at_zero(lds);
+  if (threadIdx.x < 2) reinterpret_cast<int*>(lds + (size_t)a.nt * kRegion)[threadIdx.x] = 0;
   stage_tables(lds, a.img, a.nt);
   __syncthreads();
   ib_pass<MAXD, true, false>(a, lds);

@@ -26,6 +26,14 @@ for s in $STEPS; do
         IBLDPC_LIB=$R/informationbottleneckdecodingldpc_amd/variants/libibldpc_$v.so timeout -k 10 300 python $R/bench.py --no-cpu-baseline ${AB_ARGS:-} > $O/ab_$v.json 2> $O/ab_$v.err
         rc=$?; echo "ab $v rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['avg_ms'], d['decoded_bit_errors'])" $O/ab_$v.json 2>/dev/null)" >> $O/summary.txt; crash $rc ab_$v
       done;;
+    bsweep)
+      for b in 4096 16384 32768; do
+        timeout -k 10 400 python $R/bench.py --batch-per-gpu $b --steps 3 --no-cpu-baseline > $O/bench_b$b.json 2> $O/bench_b$b.err
+        rc=$?; echo "bench B=$b rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['avg_ms'])" $O/bench_b$b.json 2>/dev/null)" >> $O/summary.txt; crash $rc bsweep
+      done;;
+    trace)
+      IBL_TRACE_WAVES=$O/trace timeout -k 10 300 python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.json 2> $O/bench_trace.err
+      rc=$?; echo "trace rc=$rc" >> $O/summary.txt; crash $rc trace;;
     mrank)
       # N>1 bench path rehearsal on one GPU: 2 ranks sharing cuda:0 over gloo
       IBL_SHARE_DEVICE=1 IBL_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_2rank.json 2> $O/bench_2rank.err
