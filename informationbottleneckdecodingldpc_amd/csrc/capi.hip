@@ -633,9 +633,9 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess)
     return bail(fail(IBL_EHIP, "hipMemset failed"));
   int bpc = 0;
-  if (fl_occupancy(0, kind, precision, g->dcm, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  if (fl_occupancy(0, kind, precision, g->dcm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_cn = bpc * g->num_cus;
-  if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 4;
+  if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_vn = bpc * g->num_cus;
   *out = h;
   return IBL_OK;

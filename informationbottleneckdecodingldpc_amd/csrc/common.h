@@ -37,6 +37,15 @@ constexpr int kLdsBytes = 160 * 1024;
 
 enum Dtype : int32_t { kU8 = 1, kI32 = 2, kF32 = 3, kF64 = 4 };
 
+// One workgroup-wide work ticket from an LDS counter (lane 0 takes it, the wave reads it back as a
+// scalar). Persistent kernels hand each block's static item share to its waves this way: waves on a
+// SIMD issue oldest-first, so equal static per-wave shares leave a CU waiting for its youngest waves.
+__device__ __forceinline__ int take_ticket(int* ctr, int lane) {
+  int t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane(t);
+}
+
 // ---------------------------------------------------------------- IB fast path
 struct IbFastArgs {
   const uint8_t* in;        // own-order inbox (nullptr for CN pass 0: inputs gathered from ch8)
@@ -156,5 +165,6 @@ hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid,
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
+int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
 
 }  // namespace ibl

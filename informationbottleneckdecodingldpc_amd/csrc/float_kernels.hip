@@ -188,17 +188,33 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 
 // MAXD = largest degree with a body in the switch (8 or 16): the registers of the degree-16 bodies
 // would cap every launch's occupancy, so codes with degrees <= 8 get their own instantiation.
+// 1024-thread blocks (512 for the MAXD=16 bodies' registers): a CU's waves share one work counter.
+// (fp64 box-plus bodies also need more than 128 VGPRs: 512 threads)
+template <int MAXD, int KIND = 0, typename F = float>
+constexpr int fl_block_of() { return (MAXD <= 8 && !(KIND == 1 && sizeof(F) == 8)) ? 1024 : 512; }
+
+// Items (node, chunk) are dealt to blocks round-robin ({b*wpb + w + nw*i}) and handed to the
+// block's waves by LDS tickets (take_ticket): ticket k -> item b*wpb + k % wpb + nw * (k / wpb).
+__device__ __forceinline__ int fl_next_item(int* ctr, int lane, int wpb, int nw) {
+  const int k = take_ticket(ctr, lane);
+  return (int)blockIdx.x * wpb + (k % wpb) + nw * (k / wpb);
+}
+
 template <int KIND, typename F, int MAXD>
-__global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
+__global__ __launch_bounds__((fl_block_of<MAXD, KIND, F>())) void fl_cn(FlArgs a) {
   const int lane = threadIdx.x & 63;
   if (!fl_gate(a.gate, lane)) return;
   constexpr int CWL = Vec<F>::N;
   constexpr int CH = 64 * CWL;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  const int nitems = a.n_nodes * a.nchunks;
   const bool do_par = a.unsat != nullptr;
   bool unsat = false;
-  for (int item = gw; item < nitems; item += nw) {
+  __shared__ int ctr;
+  if (threadIdx.x == 0) ctr = 0;
+  __syncthreads();
+  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_nodes * a.nchunks;
+  for (;;) {
+    const int item = fl_next_item(&ctr, lane, wpb, nw);
+    if (item >= nitems) break;
     const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
     const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
     const int d = a.deg[node], st = a.start[node];
@@ -211,18 +227,23 @@ __global__ __launch_bounds__(256) void fl_cn(FlArgs a) {
       default: break;
     }
   }
-  if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
+  if (do_par && __ballot(unsat) != 0ull && lane == 0)
+    atomicOr(&a.unsat[(blockIdx.x * wpb + (threadIdx.x >> 6)) & (kShards - 1)], 1);
 }
 
 template <typename F, int MAXD>
-__global__ __launch_bounds__(256) void fl_vn(FlArgs a) {
+__global__ __launch_bounds__(fl_block_of<MAXD>()) void fl_vn(FlArgs a) {
   const int lane = threadIdx.x & 63;
   if (!fl_gate(a.gate, lane)) return;
   constexpr int CWL = Vec<F>::N;
   constexpr int CH = 64 * CWL;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  const int nitems = a.n_nodes * a.nchunks;
-  for (int item = gw; item < nitems; item += nw) {
+  __shared__ int ctr;
+  if (threadIdx.x == 0) ctr = 0;
+  __syncthreads();
+  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_nodes * a.nchunks;
+  for (;;) {
+    const int item = fl_next_item(&ctr, lane, wpb, nw);
+    if (item >= nitems) break;
     const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
     const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
     const int d = a.deg[node], st = a.start[node];
@@ -325,16 +346,21 @@ static const void* fl_kernel(int which, int kind, int prec, int maxd) {
              : (small ? (const void*)fl_vn<double, 8> : (const void*)fl_vn<double, 16>);
 }
 
+int fl_block(int which, int kind, int prec, int maxd) {
+  if (which == 0 && kind == 1 && prec == kF64) return maxd <= 8 ? fl_block_of<8, 1, double>() : fl_block_of<16, 1, double>();
+  return maxd <= 8 ? fl_block_of<8>() : fl_block_of<16>();
+}
+
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s) {
   FlArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_kernel(0, kind, prec, maxd), dim3(grid), dim3(256), p, 0, s);
+  return hipLaunchKernel(fl_kernel(0, kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd)), p, 0, s);
 }
 
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s) {
   FlArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(256), p, 0, s);
+  return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(fl_block(1, 0, prec, maxd)), p, 0, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
@@ -344,7 +370,8 @@ hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) 
 }
 
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fl_kernel(which, kind, prec, maxd), 256, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fl_kernel(which, kind, prec, maxd),
+                                                      fl_block(which, kind, prec, maxd), 0);
 }
 
 }  // namespace ibl

@@ -362,13 +362,6 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch). Positions are
 // heaviest-first: [0, n_heavy) run with a MAXD-row item buffer, the rest with a kLightD-row one
 // (a degree-2 node then issues 4 row loads, not MAXD).
-// one workgroup-wide ticket (lane 0 takes it, the wave reads it back as a scalar)
-__device__ __forceinline__ int take_ticket(int* ctr, int lane) {
-  int t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __builtin_amdgcn_readfirstlane(t);
-}
-
 template <class Buf, bool VN, bool GATHER, int DLO>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, int lane, int first, int end, int nw,
                                          int wpb, int* ctr, bool do_par, bool& unsat, int& items_done) {
