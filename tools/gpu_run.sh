@@ -46,6 +46,11 @@ for s in $STEPS; do
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 3 > $O/bench_prof.json 2> $O/prof.err)
       rc=$?; echo "rocprof rc=$rc" >> $O/summary.txt; crash $rc rocprof;;
+    proffloat)
+      for k in minsum bp; do
+        (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$k -o run --output-format csv -- python3 $R/bench.py --kind $k --no-cpu-baseline --steps 2 > $O/bench_prof_$k.json 2> $O/prof_$k.err)
+        rc=$?; echo "rocprof $k rc=$rc" >> $O/summary.txt; crash $rc rocprof_$k
+      done;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/bench_pmc_$c.json 2> $O/pmc_$c.err)
