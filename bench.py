@@ -2,6 +2,12 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B] [--imax I]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+    python bench.py --config C2|C3|C5                      (BASELINE.json's other GPU configs)
+
+Default = BASELINE config C4 (the headline metric). The other presets measure the remaining GPU
+configs of BASELINE.json: C2 regular (3,6) N=8000 IB T=16 i_max=50, 65536 codewords; C3 WLAN
+N=1944 (802.11n-structured, Z=81) min-sum fp32 i_max=50, 262144 codewords; C5 DVB-S2 BP fp32
+i_max=100, 8192 codewords per GPU.
 
 A "step" = one decode call of B codewords per GPU (DVB-S2-structured N=64800 R=1/2 code,
 T=16 lookup tables with matching, i_max=50 fixed iterations — early stop off, as the roofline
@@ -39,11 +45,33 @@ def parse():
     p.add_argument("--imax", type=int, default=50)
     p.add_argument("--ebn0", type=float, default=0.6)
     p.add_argument("--kind", choices=["ib", "minsum", "bp"], default="ib")
+    p.add_argument("--code", choices=["dvbs2", "regular", "wlan"], default="dvbs2")
+    p.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default=None,
+                   help="BASELINE.json config preset (sets --code/--kind/--imax/--batch-per-gpu)")
     p.add_argument("--no-match", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=448, help="codewords of the CPU-baseline sample (~15 s on 16 host threads)")
+    p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return p.parse_args()
+    a = p.parse_args()
+    presets = {"C2": ("regular", "ib", 50, 65536), "C3": ("wlan", "minsum", 50, 262144),
+               "C4": ("dvbs2", "ib", 50, 8192), "C5": ("dvbs2", "bp", 100, 8192)}
+    if a.config:
+        a.code, a.kind, a.imax, a.batch_per_gpu = presets[a.config]
+    return a
+
+
+CODES = {"dvbs2": ("DVB-S2 N=64800 R=1/2", "DVB-S2-structured R=1/2 code (EN 302 307 profile, synthetic addresses)"),
+         "regular": ("regular (3,6) N=8000", "seeded (3,6)-regular N=8000 code (stands in for MacKay 8000.4000.3.483)"),
+         "wlan": ("WLAN 802.11n N=1944 R=1/2", "802.11n R=1/2 base matrix lifted with Z=81 (WLAN-structured)")}
+
+
+def make_code(name):
+    from informationbottleneckdecodingldpc_amd import codes
+    if name == "dvbs2":
+        return codes.dvbs2_structured(seed=0)
+    if name == "regular":
+        return codes.regular_code(8000, 3, 6, seed=0)
+    return codes.wlan_80211n(81)
 
 
 def bytes_per_cw(n_e: int, n_v: int, imax: int, w: int) -> int:
@@ -66,7 +94,7 @@ def main():
 
     # ---- setup: rank 0 builds H + tables, one broadcast to every rank (RCCL over xGMI)
     if rank == 0:
-        H = codes.dvbs2_structured(seed=0)
+        H = make_code(a.code)
         g0 = graph.build_graph(H)
         tb0 = tables.random_tables(16, 16, g0.d_c_max, g0.d_v_max, I, seed=1)
         arrays = dict(indptr=g0.csr_indptr, cols=g0.csr_cols, shape=np.array([g0.n_c, g0.n_v]),
@@ -174,25 +202,47 @@ def main():
         lds = {k: round(lk[k] / (avg[k] * 1e-3) / (256 * 2.4e9), 2) for k in lk}
         lds["ceiling"] = 32.0
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.kind == "ib":
+    code_name, code_desc = CODES[a.code]
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle
         nthreads = min(16, os.cpu_count() or 1)
-        S = a.cpu_sample
-        ch_cpu = ch[:, :S].cpu().numpy().astype(np.int32)
-        tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+        # bounded sample: a 16-codeword calibration run sizes the measured sample to ~12 s of CPU work
+        # (--cpu-sample caps it)
+        if a.kind == "ib":
+            tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+            dec_cpu = lambda x: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nthreads)  # noqa: E731
+            src = ch
+        else:
+            dec_cpu = lambda x: oracle.float_decode(g, 0 if a.kind == "minsum" else 1, I, x,  # noqa: E731
+                                                    early_stop=False, nthreads=nthreads)
+            src = llr
+        host = (lambda S_: src[:, :S_].cpu().numpy().astype(np.int32 if a.kind == "ib" else np.float64))  # noqa: E731
+        S0 = min(16, B)
         t1 = time.perf_counter()
-        ref = oracle.ib_decode(g, tbh, ch_cpu, match=match, early_stop=False, nthreads=nthreads)
+        dec_cpu(host(S0))
+        cal = time.perf_counter() - t1
+        S = int(max(S0, min(B, a.cpu_sample, S0 * 12.0 / max(cal, 1e-3))))
+        x_cpu = host(S)
+        t1 = time.perf_counter()
+        ref = dec_cpu(x_cpu)
         cpu_s = time.perf_counter() - t1
-        same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int32)))
+        if a.kind == "ib":
+            same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int32)))
+            what = (f"oracle/ib_oracle.c (C+OpenMP restatement of the reference OpenCL kernels; the reference's "
+                    f"own numpy host path cannot decode DVB-S2); outputs equal GPU: {same}")
+        else:
+            agree = float(np.mean((ref < 0) == (out[:, :S].cpu().numpy() < 0)))
+            what = (f"oracle/ib_oracle.c fp64 restatement of kernels_min_and_BP.cl (the reference's float host "
+                    f"paths are broken, SURVEY App. C3); hard decisions equal to the GPU's fp32: {agree:.6f}")
         cpu = {"value": round(S / cpu_s, 3), "unit": "codewords/s", "cores": nthreads, "kind": "port",
-               "sample": f"{S} of the benchmark's codewords, DVB-S2 N=64800, i_max={I}, matching on, fixed "
-                         f"iterations; oracle/ib_oracle.c (C+OpenMP restatement of the reference OpenCL kernels; "
-                         f"the reference's own numpy host path cannot decode DVB-S2), {cpu_s:.1f} s wall; "
-                         f"outputs equal GPU: {same}"}
+               "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, fixed iterations; {what}; "
+                         f"{cpu_s:.1f} s wall"}
 
     if rank == 0:
         line = {
-            "metric": "decoded codewords/sec + achieved HBM GB/s, DVB-S2 N=64800 i_max=50",
+            "metric": ("decoded codewords/sec + achieved HBM GB/s, DVB-S2 N=64800 i_max=50"
+                       if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else
+                       f"decoded codewords/sec + achieved HBM GB/s, {code_name} {a.kind} i_max={I}"),
             "value": round(value, 1),
             "unit": "codewords/s",
             "n_gpus": world,
@@ -204,11 +254,12 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": f"synthetic: all-zero codeword, BPSK/AWGN at Eb/N0 {a.ebn0} dB quantised to 16 clusters; "
-                    f"random T=16 IB tables; DVB-S2-structured R=1/2 code (EN 302 307 profile, synthetic addresses)",
-            "config": {"workload": f"DVB-S2 N=64800 R=1/2, "
+                    f"{'random T=16 IB tables' if a.kind == 'ib' else 'cluster LLRs'}; {code_desc}",
+            "config": {"workload": f"{code_name}, "
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, matching {'on' if match else 'off'}, fixed iterations",
-                       "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split"},
+                       "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
+                       "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
             "hbm_gbps_algorithmic": round(value * bpc / 1e9, 1),
             "bytes_per_codeword": bpc,
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,

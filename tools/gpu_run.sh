@@ -34,6 +34,11 @@ for s in $STEPS; do
     trace)
       IBL_TRACE_WAVES=$O/trace timeout -k 10 300 python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.json 2> $O/bench_trace.err
       rc=$?; echo "trace rc=$rc" >> $O/summary.txt; crash $rc trace;;
+    configs)
+      for c in C2 C3 C5; do
+        timeout -k 10 600 python $R/bench.py --config $c --steps 3 > $O/bench_$c.json 2> $O/bench_$c.err
+        rc=$?; echo "bench $c rc=$rc $(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['roofline']['avg_ms'], d['roofline']['frac'], d['cpu_baseline']['value'] if d['cpu_baseline'] else None)" $O/bench_$c.json 2>/dev/null)" >> $O/summary.txt; crash $rc bench_$c
+      done;;
     mrank)
       # N>1 bench path rehearsal on one GPU: 2 ranks sharing cuda:0 over gloo
       IBL_SHARE_DEVICE=1 IBL_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_2rank.json 2> $O/bench_2rank.err
