@@ -633,10 +633,12 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess)
     return bail(fail(IBL_EHIP, "hipMemset failed"));
   int bpc = 0;
+  // at most 16 waves per CU: with a second block per CU its waves issue behind the first block's
+  // (oldest-first) and the per-block work counters cannot rebalance across blocks
   if (fl_occupancy(0, kind, precision, g->dcm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
-  h->grid_cn = bpc * g->num_cus;
+  h->grid_cn = std::min(bpc, 1024 / fl_block(0, kind, precision, g->dcm)) * g->num_cus;
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
-  h->grid_vn = bpc * g->num_cus;
+  h->grid_vn = std::min(bpc, 1024 / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
   *out = h;
   return IBL_OK;
 }

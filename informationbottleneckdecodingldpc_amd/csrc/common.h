@@ -37,6 +37,12 @@ constexpr int kLdsBytes = 160 * 1024;
 
 enum Dtype : int32_t { kU8 = 1, kI32 = 2, kF32 = 3, kF64 = 4 };
 
+// Read-only graph arrays read through the constant address space: uniform indices become scalar
+// loads (the compiler cannot otherwise prove they do not alias the inbox being written, and would
+// issue vector loads whose waits drain every outstanding row load).
+typedef __attribute__((address_space(4))) const int32_t cint32;
+__device__ __forceinline__ int32_t sload(const int32_t* p, int i) { return ((cint32*)p)[i]; }
+
 // One workgroup-wide work ticket from an LDS counter (lane 0 takes it, the wave reads it back as a
 // scalar). Persistent kernels hand each block's static item share to its waves this way: waves on a
 // SIMD issue oldest-first, so equal static per-wave shares leave a CU waiting for its youngest waves.

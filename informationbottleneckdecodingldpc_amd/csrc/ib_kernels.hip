@@ -27,11 +27,6 @@
 
 namespace ibl {
 
-// Read-only graph arrays read through the constant address space: uniform indices become scalar
-// loads (the compiler cannot otherwise prove they do not alias the inbox being written, and would
-// issue vector loads whose waits drain every outstanding row load).
-typedef __attribute__((address_space(4))) const int32_t cint32;
-__device__ __forceinline__ int32_t sload(const int32_t* p, int i) { return ((cint32*)p)[i]; }
 
 // LDS lookups take a 32-bit LDS byte address. These kernels have no static LDS, so the dynamic
 // array starts at LDS address 0 (checked at kernel entry: lds_at_zero): a lookup is one v_lshl_add
