@@ -693,8 +693,13 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   dc.vin0 = h->vbuf0; dc.vin1 = h->vbuf1; dc.ch = h->chf; dc.start = g->vn_start; dc.deg = g->vn_deg;
   dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.n_nodes = g->n_v; dc.nchunks = nchunks;
   dc.ldb = h->ldb; dc.B = B;
-  const size_t total = (size_t)g->n_v * B;
-  HIPCHK(launch_fl_dec(dc, h->prec, (int)std::min<size_t>((total + 255) / 256, 8192), s));
+  {
+    const int n_per = h->prec == kF32 ? 4 : 2;                      // codewords per lane
+    const size_t esz = out_dtype == kF32 ? 4 : 8;
+    dc.aligned = ((B % n_per) == 0 && ((uintptr_t)d_out % (n_per * esz)) == 0) ? 1 : 0;
+    const size_t items = (size_t)g->n_v * nchunks;
+    HIPCHK(launch_fl_dec(dc, h->prec, (int)std::min<size_t>((items + 3) / 4, 65536), s));
+  }
   return IBL_OK;
 }
 

@@ -337,22 +337,58 @@ __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
   }
 }
 
-// APP LLR = ch + sum of all inputs in ascending order, unclamped (kernels_min_and_BP.cl:196-202)
+// APP LLR = ch + sum of all inputs in ascending order, unclamped (kernels_min_and_BP.cl:196-202).
+// Wave item = (node, chunk of 64*N codewords); vector loads of every edge row, vector stores when the
+// user buffer is aligned (scalar tail otherwise).
 template <typename F>
 __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
+  using V = Vec<F>;
+  constexpr int N = V::N, CH = 64 * N;
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
   const F* vin = reinterpret_cast<const F*>((L & 1) ? a.vin1 : a.vin0);
   const F* ch = reinterpret_cast<const F*>(a.ch);
-  const size_t total = (size_t)a.n_nodes * a.B;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int n = (int)(i / a.B);
-    const int b = (int)(i - (size_t)n * a.B);
-    const int d = a.deg[n], st = a.start[n];
-    F x = ch[(size_t)n * a.ldb + b];
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+  const int nitems = a.n_nodes * a.nchunks;
+  for (int item = gw; item < nitems; item += nw) {
+    const int n = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+    const int chunk = __builtin_amdgcn_readfirstlane(item - n * a.nchunks);
+    const int cw0 = chunk * CH + lane * N;
+    if (cw0 >= a.B) continue;
+    const int d = sload(a.deg, n), st = sload(a.start, n);
+    F x[N];
+    {
+      const typename V::T r = *reinterpret_cast<const typename V::T*>(ch + (size_t)n * a.ldb + cw0);
+#pragma unroll
+      for (int s = 0; s < N; ++s) x[s] = V::get(r, s);
+    }
     if (L > 0)
-      for (int v = 0; v < d; ++v) x = x + vin[(size_t)(st + v) * a.ldb + b];
-    if (a.out_dtype == kF32) reinterpret_cast<float*>(a.out)[i] = (float)x;
-    else reinterpret_cast<double*>(a.out)[i] = (double)x;
+      for (int v = 0; v < d; ++v) {
+        const typename V::T r = *reinterpret_cast<const typename V::T*>(vin + (size_t)(st + v) * a.ldb + cw0);
+#pragma unroll
+        for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
+      }
+    const size_t o = (size_t)n * a.B + cw0;
+    if (a.out_dtype == kF32) {
+      float* p = reinterpret_cast<float*>(a.out) + o;
+      if (a.aligned && cw0 + N <= a.B) {
+        if constexpr (N == 4) *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+        else *reinterpret_cast<float2*>(p) = make_float2((float)x[0], (float)x[1]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < N; ++s)
+          if (cw0 + s < a.B) p[s] = (float)x[s];
+      }
+    } else {
+      double* p = reinterpret_cast<double*>(a.out) + o;
+      if (a.aligned && cw0 + N <= a.B && N == 2) {
+        *reinterpret_cast<double2*>(p) = make_double2((double)x[0], (double)x[1]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < N; ++s)
+          if (cw0 + s < a.B) p[s] = (double)x[s];
+      }
+    }
   }
 }
 
