@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define IBL_VERSION 2
+#define IBL_VERSION 3
 
 enum { IBL_OK = 0, IBL_EINVAL = -1, IBL_EHIP = -2, IBL_ENOMEM = -3, IBL_EUNSUPPORTED = -4 };
 enum { IBL_U8 = 1, IBL_I32 = 2, IBL_F32 = 3, IBL_F64 = 4 };
@@ -151,6 +151,38 @@ int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int
  */
 int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t seed, uint64_t offset, int32_t n,
                        int32_t B, const uint8_t* d_bits, void* d_out, int32_t out_dtype, int64_t ld, void* stream);
+
+/* ---- LDPC encoding ------------------------------------------------------
+ * Batched systematic encoder, replacing Discrete_LDPC_decoding/LDPC_encoder.py: the plan that
+ * getLDPCEncoderParamters (:197-269) derives from H = [A | B] (B triangular with a full diagonal,
+ * possibly after reversing its rows -> forward/backward substitution; else GF(2) factorisation
+ * gf2factorize :287-340 with its first-candidate pivot rule -> "Matrix Inverse") is built natively
+ * from H's canonical CSR (sorted columns); encode (:86-123) / encode_c (:125-162) run for B
+ * codewords at once, 32 codewords per dword. A bidiagonal substitution (DVB-S2 IRA parity) runs as a
+ * segmented prefix-XOR scan. Returns IBL_EINVAL when B is singular in GF(2) (the reference raises).
+ */
+typedef struct ibl_encoder ibl_encoder;
+int ibl_encoder_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int32_t* cols, int32_t max_batch,
+                       int32_t device, ibl_encoder** out);
+/* "Forward Substitution" | "Backward Substitution" | "Matrix Inverse" (EncodingAlgorithm, :269) */
+const char* ibl_encoder_algorithm(const ibl_encoder* h);
+/* d_info: u8 [K][B] information bits (0/1), d_code: u8 [N][B] codewords [info; parity]
+ * (LDPC_Transmitter.py transmit :109-125 encodes msg_at_time columns one by one). */
+int ibl_encode(ibl_encoder* h, const uint8_t* d_info, int32_t B, uint8_t* d_code, void* stream);
+void ibl_encoder_destroy(ibl_encoder* h);
+
+/* Random information bits u8 [n][B] (np.random.randint(0, 2, (data_len, msg_at_time)) in
+ * LDPC_Transmitter.py:111): bit i = top bit of the i-th 64-bit output of numpy's Philox4x64-10
+ * stream with key (seed, 0) advanced by `offset` blocks (Generator(Philox(key=seed)).advance(offset)
+ * .random_raw(n*B) >> 63); the next batch uses offset += ceil(n*B/4). */
+int ibl_random_bits(uint64_t seed, uint64_t offset, int32_t n, int32_t B, uint8_t* d_out, void* stream);
+
+/* Bit errors of decoder output against transmitted bits: *d_count = #{(r,b): r < rows, b < B,
+ * (x[r*ld+b] < threshold) != (bits[r*bits_ld+b] != 0)} as int64 (generalises
+ * return_errors_all_zero, Discrete_LDPC_decoding/discrete_LDPC_decoder_irreg.py:343-349, to non-zero codewords;
+ * threshold T/2 for cluster ids, 0 for LLRs). x dtype: IBL_U8/IBL_I32/IBL_F32/IBL_F64. */
+int ibl_count_errors(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
+                     const uint8_t* d_bits, int64_t bits_ld, int64_t* d_count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libibldpc.so")
-SOURCES = ["ib_kernels.hip", "float_kernels.hip", "channel_kernels.hip", "capi.hip"]
+SOURCES = ["ib_kernels.hip", "float_kernels.hip", "channel_kernels.hip", "encoder_kernels.hip", "capi.hip"]
 ARCH = os.environ.get("IBLDPC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,

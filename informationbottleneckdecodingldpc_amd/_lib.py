@@ -29,6 +29,12 @@ EXPORTS = [
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
     "ibl_ib_timing", "ibl_ib_timing_read", "ibl_float_timing", "ibl_float_timing_read",
     "ibl_channel_sample",
+    "ibl_encoder_create",
+    "ibl_encoder_algorithm",
+    "ibl_encode",
+    "ibl_encoder_destroy",
+    "ibl_random_bits",
+    "ibl_count_errors",
 ]
 
 
@@ -79,6 +85,14 @@ def load():
     _dp = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
     L.ibl_channel_sample.argtypes = [_dp, _i32, _vp, ctypes.c_uint64, ctypes.c_uint64, _i32, _i32, _vp, _vp,
                                      _i32, _i64, _vp]
+    L.ibl_encoder_create.argtypes = [_i32, _i32, _i32p, _i32p, _i32, _i32, ctypes.POINTER(_vp)]
+    L.ibl_encoder_algorithm.argtypes = [_vp]
+    L.ibl_encoder_algorithm.restype = ctypes.c_char_p
+    L.ibl_encode.argtypes = [_vp, _vp, _i32, _vp, _vp]
+    L.ibl_encoder_destroy.argtypes = [_vp]
+    L.ibl_encoder_destroy.restype = None
+    L.ibl_random_bits.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _i32, _i32, _vp, _vp]
+    L.ibl_count_errors.argtypes = [_vp, _i32, _i64, _i32, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     for name in EXPORTS:
         getattr(L, name)
     _lib = L

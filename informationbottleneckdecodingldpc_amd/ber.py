@@ -15,6 +15,12 @@ Multi-GPU: one process per GPU (torch.distributed initialised by the caller); ra
 channel from Philox key ``seed + r`` (disjoint streams), and the error / block counters are summed
 over ranks (one small all-reduce per ``sync_every`` batches) so every rank stops at the same point.
 ``max_blocks`` bounds a point (the reference loops until ``min_errors`` however long that takes).
+
+``encoded=True`` transmits random encoded codewords instead (the reference's
+``LDPC_BPSK_Transmitter`` + encoder path, AWGN_Channel_Transmission/LDPC_Transmitter.py:109-125): bits
+from the device Philox stream (key ``seed + rank``), batched device encoding, the channel mirrored by
+the codeword bits, and decided bits compared with the transmitted ones (``ibl_count_errors``) over the
+rows ``return_errors_all_zero`` counts.
 """
 from __future__ import annotations
 
@@ -45,6 +51,7 @@ class BERConfig:
     seed: int = 0
     sync_every: int = 1                   # batches between cross-rank counter reductions
     llr_dtype: Optional[object] = None    # float decoders: torch dtype of the channel LLRs
+    encoded: bool = False                 # random encoded codewords (LDPC_BPSK_Transmitter) instead of all-zero
 
 
 @dataclass
@@ -113,6 +120,17 @@ def run_ber(decoder, cfg: BERConfig, quantizer_factory: Optional[Callable] = Non
     ber: List[float] = [0.0]
     res = BERResult(np.array([]), np.array([]))
     offset = 0
+    tx = None
+    if cfg.encoded:
+        import torch
+        from .engine import count_errors
+        from .ldpc_encoder import LDPC_BPSK_Transmitter
+        tx = LDPC_BPSK_Transmitter(decoder.H_sparse, cfg.msg_at_time, seed=int(cfg.seed) + rank,
+                                   device=getattr(decoder, "device", None))
+        # rows return_errors_all_zero counts: all N for the regular IB class (:297-300), data_len otherwise
+        err_rows = N_var if type(decoder).__name__ == "Discrete_LDPC_Decoder_class" else int(decoder.data_len)
+        thr = decoder.cardinality_T_decoder_ops // 2 if kind == "ib" else 0.0
+        cnt = torch.zeros(1, dtype=torch.int64, device=tx.encoder.device)
     while True:
         EbN0_dB = ebn0[-1]
         sigma_n2 = 10 ** (-EbN0_dB / 10) / (2 * R_c)
@@ -128,14 +146,18 @@ def run_ber(decoder, cfg: BERConfig, quantizer_factory: Optional[Callable] = Non
         nb = 0
         t0 = time.time()
         while errors < cfg.min_errors and (cfg.max_blocks is None or blocks < cfg.max_blocks):
+            kw = {} if tx is None else {"bits": tx.transmit_bits()}
             if kind == "ib":
-                rec = quanti.quantize_direct_OpenCL(N_var, cfg.msg_at_time)
+                rec = quanti.quantize_direct_OpenCL(N_var, cfg.msg_at_time, **kw)
                 dec = decoder.decode_OpenCL(rec, buffer_in=True, return_buffer=True)
             else:
-                rec = quanti.quantize_direct_OpenCL_LLR(N_var, cfg.msg_at_time, dtype=cfg.llr_dtype)
+                rec = quanti.quantize_direct_OpenCL_LLR(N_var, cfg.msg_at_time, dtype=cfg.llr_dtype, **kw)
                 fn = decoder.decode_OpenCL_min_sum if kind == "minsum" else decoder.decode_OpenCL_belief_propagation
                 dec = fn(rec, buffer_in=True, return_buffer=True)
-            pend_err += decoder.return_errors_all_zero(dec)
+            if tx is None:
+                pend_err += decoder.return_errors_all_zero(dec)
+            else:
+                pend_err += int(count_errors(dec.contiguous(), err_rows, thr, kw["bits"], cnt).item())
             pend_blk += cfg.msg_at_time
             nb += 1
             if nb % max(1, cfg.sync_every) == 0:

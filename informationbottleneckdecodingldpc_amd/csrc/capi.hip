@@ -731,6 +731,219 @@ int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t
   return IBL_OK;
 }
 
+// ------------------------------------------------------------------ encoder
+}  // extern "C"
+
+struct ibl_encoder {
+  int device = 0;
+  int32_t N = 0, K = 0, M = 0, max_batch = 0, Bw = 0, method = 0, dir = 1, chain = 0;
+  std::string algo;
+  int32_t *a_ip = nullptr, *a_ix = nullptr, *l_ip = nullptr, *l_ix = nullptr, *p_ip = nullptr, *p_ix = nullptr;
+  int32_t* order = nullptr;
+  uint32_t *x = nullptr, *r = nullptr, *t = nullptr, *p = nullptr, *tot = nullptr;
+};
+
+namespace {
+struct Csr {
+  std::vector<int32_t> ip{0}, ix;
+  void push_row(const std::vector<int32_t>& cols) {
+    ix.insert(ix.end(), cols.begin(), cols.end());
+    ip.push_back((int32_t)ix.size());
+  }
+};
+
+// 1 lower / -1 upper triangular with full diagonal, 0 otherwise (LDPC_encoder.py:342-360);
+// rows given as sorted column lists of the square parity part
+int tri_shape(const std::vector<std::vector<int32_t>>& rows) {
+  const int n = (int)rows.size();
+  int64_t nnz = 0, low = 0;
+  for (int i = 0; i < n; ++i) {
+    bool diag = false;
+    for (int c : rows[i]) {
+      ++nnz;
+      if (c <= i) ++low;
+      if (c == i) diag = true;
+    }
+    if (!diag) return 0;
+  }
+  if (low == nnz) return 1;
+  if (low == n) return -1;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int ibl_encoder_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int32_t* cols, int32_t max_batch,
+                       int32_t device, ibl_encoder** out) {
+  if (!out) return fail(IBL_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n_v <= n_c || n_c <= 0) return fail(IBL_EINVAL, "H must have fewer rows than columns");
+  if (max_batch < 1) return fail(IBL_EINVAL, "max_batch must be >= 1");
+  const int32_t N = n_v, M = n_c, K = N - M;
+  HIPCHK(hipSetDevice(device));
+  // H = [A | B]; rows of B as column lists relative to K (H is canonical CSR, sorted columns)
+  std::vector<std::vector<int32_t>> brows(M);
+  Csr A;
+  for (int32_t r = 0; r < M; ++r) {
+    std::vector<int32_t> ac;
+    for (int32_t e = indptr[r]; e < indptr[r + 1]; ++e) {
+      const int32_t c = cols[e];
+      if (c < 0 || c >= N) return fail(IBL_EINVAL, "column index out of range");
+      if (c < K) ac.push_back(c); else brows[r].push_back(c - K);
+    }
+    A.push_row(ac);
+  }
+  auto* h = new ibl_encoder();
+  h->device = device; h->N = N; h->K = K; h->M = M; h->max_batch = max_batch;
+  h->Bw = (max_batch + 31) / 32;
+  std::vector<int32_t> order;
+  Csr L, P;
+  auto strict = [&](const std::vector<std::vector<int32_t>>& rows, int dir) {
+    Csr T;
+    for (int i = 0; i < (int)rows.size(); ++i) {
+      std::vector<int32_t> c;
+      for (int j : rows[i])
+        if (dir > 0 ? j < i : j > i) c.push_back(j);
+      T.push_row(c);
+    }
+    return T;
+  };
+  int shape = tri_shape(brows);
+  if (shape != 0) {                                    // (LDPC_encoder.py:208-213)
+    h->algo = shape == 1 ? "Forward Substitution" : "Backward Substitution";
+    h->dir = shape;
+    P = strict(brows, shape);
+  } else {
+    std::vector<std::vector<int32_t>> rev(brows.rbegin(), brows.rend());
+    const int rshape = tri_shape(rev);
+    if (rshape != 0) {                                 // rows reversed (:214-226)
+      h->algo = rshape == 1 ? "Forward Substitution" : "Backward Substitution";
+      h->dir = rshape;
+      for (int i = 0; i < M; ++i) order.push_back(M - 1 - i);
+      P = strict(rev, rshape);
+    } else {                                           // GF(2) factorisation (:227-246, gf2factorize :287-340)
+      if (M > 16384) { delete h; return fail(IBL_EUNSUPPORTED, "GF(2) factorisation limited to 16384 parity bits"); }
+      h->algo = "Matrix Inverse";
+      h->method = 1;
+      const int words = (M + 63) / 64;
+      std::vector<uint64_t> Y2((size_t)M * words, 0), Y1((size_t)M * words, 0);
+      for (int i = 0; i < M; ++i) {
+        for (int c : brows[i]) Y2[(size_t)i * words + (c >> 6)] |= 1ull << (c & 63);
+        Y1[(size_t)i * words + (i >> 6)] |= 1ull << (i & 63);
+      }
+      std::vector<char> used(M, 0);
+      std::vector<int32_t> piv(M, 0);
+      for (int col = 0; col < M; ++col) {
+        const uint64_t bit = 1ull << (col & 63);
+        int pv = -1;
+        for (int i = 0; i < M; ++i)
+          if (!used[i] && (Y2[(size_t)i * words + (col >> 6)] & bit)) {
+            if (pv < 0) { pv = i; continue; }
+            for (int w = 0; w < words; ++w) Y2[(size_t)i * words + w] ^= Y2[(size_t)pv * words + w];
+            Y1[(size_t)i * words + (pv >> 6)] |= 1ull << (pv & 63);
+          }
+        if (pv < 0) { delete h; return fail(IBL_EINVAL, "the last N-K columns of H are singular in GF(2)"); }
+        used[pv] = 1;
+        piv[col] = pv;
+      }
+      auto row_cols = [&](const std::vector<uint64_t>& Y, int i) {
+        std::vector<int32_t> c;
+        for (int w = 0; w < words; ++w)
+          for (uint64_t v = Y[(size_t)i * words + w]; v; v &= v - 1) c.push_back(w * 64 + __builtin_ctzll(v));
+        return c;
+      };
+      std::vector<std::vector<int32_t>> l(M), u(M);
+      for (int i = 0; i < M; ++i) {
+        l[i] = row_cols(Y1, i);
+        u[i] = row_cols(Y2, piv[i]);
+      }
+      L = strict(l, 1);
+      P = strict(u, -1);
+      h->dir = -1;
+      order = piv;
+    }
+  }
+  // bidiagonal P in substitution order -> prefix-XOR scan
+  bool chain = true;
+  for (int i = 0; i < M && chain; ++i) {
+    const int n = P.ip[i + 1] - P.ip[i];
+    const int want = h->dir > 0 ? i - 1 : i + 1;
+    if (want < 0 || want >= M) chain = n == 0;
+    else chain = n == 1 && P.ix[P.ip[i]] == want;
+  }
+  h->chain = chain ? 1 : 0;
+  auto bail = [&](int rc) { ibl_encoder_destroy(h); return rc; };
+  int rc;
+  if ((rc = dupload(&h->a_ip, A.ip.data(), A.ip.size())) || (rc = dupload(&h->a_ix, A.ix.data(), A.ix.size())) ||
+      (rc = dupload(&h->p_ip, P.ip.data(), P.ip.size())) || (rc = dupload(&h->p_ix, P.ix.data(), P.ix.size())))
+    return bail(rc);
+  if (h->method == 1 && ((rc = dupload(&h->l_ip, L.ip.data(), L.ip.size())) || (rc = dupload(&h->l_ix, L.ix.data(), L.ix.size()))))
+    return bail(rc);
+  if (!order.empty() && (rc = dupload(&h->order, order.data(), order.size()))) return bail(rc);
+  const size_t wm = (size_t)M * h->Bw;
+  if ((rc = dalloc(&h->x, (size_t)K * h->Bw)) || (rc = dalloc(&h->r, wm)) || (rc = dalloc(&h->t, wm)) ||
+      (rc = dalloc(&h->p, wm)) || (rc = dalloc(&h->tot, (size_t)enc_scan_segments() * h->Bw)))
+    return bail(rc);
+  *out = h;
+  return IBL_OK;
+}
+
+const char* ibl_encoder_algorithm(const ibl_encoder* h) { return h ? h->algo.c_str() : ""; }
+
+int ibl_encode(ibl_encoder* h, const uint8_t* d_info, int32_t B, uint8_t* d_code, void* stream) {
+  if (!h) return fail(IBL_EINVAL, "encoder is NULL");
+  if (B < 1 || B > h->max_batch) return fail(IBL_EINVAL, "B must lie in [1, max_batch]");
+  if (!d_info || !d_code) return fail(IBL_EINVAL, "NULL buffer");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(h->device));
+  const int Bw = (B + 31) / 32, M = h->M;
+  HIPCHK(launch_enc_pack(d_info, h->K, B, Bw, h->x, s));
+  HIPCHK(launch_enc_ax(h->x, h->a_ip, h->a_ix, M, Bw, h->r, s));
+  uint32_t* cur = h->r;
+  if (h->method == 1) {                                 // L substitution (forward), then row order
+    HIPCHK(launch_enc_subst(cur, h->t, h->l_ip, h->l_ix, M, Bw, 1, s));
+    cur = h->t;
+  }
+  if (h->order) {
+    uint32_t* dst = cur == h->r ? h->t : h->r;
+    HIPCHK(launch_enc_gather(cur, h->order, M, Bw, dst, s));
+    cur = dst;
+  }
+  if (h->chain) HIPCHK(launch_enc_scan(cur, h->tot, M, Bw, h->dir, h->p, s));
+  else HIPCHK(launch_enc_subst(cur, h->p, h->p_ip, h->p_ix, M, Bw, h->dir, s));
+  HIPCHK(launch_enc_unpack(d_info, h->p, h->K, M, B, Bw, d_code, s));
+  return IBL_OK;
+}
+
+void ibl_encoder_destroy(ibl_encoder* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  dfree(h->a_ip); dfree(h->a_ix); dfree(h->l_ip); dfree(h->l_ix); dfree(h->p_ip); dfree(h->p_ix); dfree(h->order);
+  dfree(h->x); dfree(h->r); dfree(h->t); dfree(h->p); dfree(h->tot);
+  delete h;
+}
+
+int ibl_random_bits(uint64_t seed, uint64_t offset, int32_t n, int32_t B, uint8_t* d_out, void* stream) {
+  if (!d_out || n < 0 || B < 0) return fail(IBL_EINVAL, "bad arguments");
+  if ((int64_t)n * B == 0) return IBL_OK;
+  HIPCHK(launch_random_bits(seed, offset, (int64_t)n * B, d_out, (hipStream_t)stream));
+  return IBL_OK;
+}
+
+int ibl_count_errors(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
+                     const uint8_t* d_bits, int64_t bits_ld, int64_t* d_count, void* stream) {
+  if (!d_x || !d_bits || !d_count) return fail(IBL_EINVAL, "NULL buffer");
+  if (dtype != kU8 && dtype != kI32 && dtype != kF32 && dtype != kF64) return fail(IBL_EINVAL, "unknown dtype");
+  if (rows < 0 || B < 0 || ld < B || bits_ld < B) return fail(IBL_EINVAL, "bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(d_count, 0, sizeof(int64_t), s));
+  if (rows * B == 0) return IBL_OK;
+  HIPCHK(launch_count_errors(d_x, dtype, rows, B, ld, threshold, d_bits, bits_ld,
+                             reinterpret_cast<unsigned long long*>(d_count), s));
+  return IBL_OK;
+}
+
 int ibl_count_below(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
                     int64_t* d_count, void* stream) {
   if (!d_x || !d_count) return fail(IBL_EINVAL, "NULL buffer");

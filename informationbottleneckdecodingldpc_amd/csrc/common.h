@@ -162,6 +162,21 @@ struct ChArgs {
 };
 hipError_t launch_ch_sample(const ChArgs& a, hipStream_t s);
 
+// ------------------------------------------------------------------ encoder
+hipError_t launch_enc_pack(const uint8_t* in, int rows, int B, int Bw, uint32_t* out, hipStream_t s);
+hipError_t launch_enc_ax(const uint32_t* x, const int32_t* indptr, const int32_t* cols, int M, int Bw, uint32_t* r,
+                         hipStream_t s);
+hipError_t launch_enc_subst(const uint32_t* in, uint32_t* out, const int32_t* indptr, const int32_t* cols, int M,
+                            int Bw, int dir, hipStream_t s);
+hipError_t launch_enc_scan(const uint32_t* r, uint32_t* tot, int M, int Bw, int dir, uint32_t* p, hipStream_t s);
+int enc_scan_segments();
+hipError_t launch_enc_gather(const uint32_t* in, const int32_t* order, int M, int Bw, uint32_t* out, hipStream_t s);
+hipError_t launch_enc_unpack(const uint8_t* info, const uint32_t* p, int K, int M, int B, int Bw, uint8_t* code,
+                             hipStream_t s);
+hipError_t launch_random_bits(uint64_t seed, uint64_t offset, int64_t total, uint8_t* out, hipStream_t s);
+hipError_t launch_count_errors(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
+                               const uint8_t* bits, int64_t bits_ld, unsigned long long* cnt, hipStream_t s);
+
 hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
                               unsigned long long* cnt, hipStream_t s);
 

@@ -227,3 +227,74 @@ def channel_sample(out: torch.Tensor, cdf: np.ndarray, seed: int, offset: int,
                                               out.data_ptr(), _DT_ANY[out.dtype], B, _stream_ptr(out.device)),
                "ibl_channel_sample")
     return out
+
+
+class Encoder:
+    """Batched systematic LDPC encoder on one device (``ibl_encoder``; the reference's
+    Discrete_LDPC_decoding/LDPC_encoder.py plan :197-269 and encode :86-123, for B words at once)."""
+
+    def __init__(self, H, max_batch: int, device=None):
+        from .codes import canonical_csr
+        self.device = _require_gpu(device)
+        Hc = canonical_csr(H)
+        self.N_c, self.N = Hc.shape
+        self.K = self.N - self.N_c
+        self.max_batch = int(max_batch)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().ibl_encoder_create(self.N, self.N_c, np.ascontiguousarray(Hc.indptr, np.int32),
+                                                  np.ascontiguousarray(Hc.indices, np.int32), self.max_batch,
+                                                  self.device.index, ctypes.byref(h)), "ibl_encoder_create")
+        self._h = h
+        self.algorithm = _lib.load().ibl_encoder_algorithm(h).decode()
+
+    def encode(self, info: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """u8 [K][B] information bits on the device -> u8 [N][B] codewords [info; parity]."""
+        _check_tensor(info, self.device, self.K, "info")
+        if info.dtype != torch.uint8:
+            raise ValueError("info must be uint8")
+        B = info.shape[1]
+        if out is None:
+            out = torch.empty((self.N, B), dtype=torch.uint8, device=self.device)
+        _check_tensor(out, self.device, self.N, "out")
+        if out.dtype != torch.uint8 or out.shape[1] != B:
+            raise ValueError("out must be a uint8 [N][B] tensor")
+        _lib.check(_lib.load().ibl_encode(self._h, info.data_ptr(), B, out.data_ptr(), _stream_ptr(self.device)),
+                   "ibl_encode")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().ibl_encoder_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self._h = None
+
+
+def random_bits(out: torch.Tensor, seed: int, offset: int) -> torch.Tensor:
+    """Fill a contiguous u8 [n][B] device tensor with information bits from the numpy-compatible
+    Philox4x64-10 stream (top bit of each output; consumes :func:`philox_blocks` counter blocks)."""
+    if out.dim() != 2 or not out.is_contiguous() or out.device.type != "cuda" or out.dtype != torch.uint8:
+        raise ValueError("out must be a contiguous 2-D uint8 device tensor")
+    n, B = out.shape
+    _lib.check(_lib.load().ibl_random_bits(int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), n, B,
+                                           out.data_ptr(), _stream_ptr(out.device)), "ibl_random_bits")
+    return out
+
+
+def count_errors(x: torch.Tensor, rows: int, threshold: float, bits: torch.Tensor,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device count of decided bits ``x[:rows] < threshold`` that differ from ``bits[:rows]`` -> int64."""
+    if x.dim() != 2 or not x.is_contiguous() or x.device.type != "cuda" or x.dtype not in _DT_ANY:
+        raise ValueError("x must be a contiguous 2-D device tensor (uint8/int32/float32/float64)")
+    if bits.dtype != torch.uint8 or bits.dim() != 2 or not bits.is_contiguous() or bits.device != x.device \
+            or bits.shape[1] != x.shape[1]:
+        raise ValueError("bits must be a contiguous uint8 [n][B] tensor on x's device")
+    rows = min(int(rows), x.shape[0], bits.shape[0])
+    if out is None:
+        out = torch.empty(1, dtype=torch.int64, device=x.device)
+    _lib.check(_lib.load().ibl_count_errors(x.data_ptr(), _DT_ANY[x.dtype], rows, x.shape[1], x.shape[1],
+                                            float(threshold), bits.data_ptr(), bits.shape[1], out.data_ptr(),
+                                            _stream_ptr(x.device)), "ibl_count_errors")
+    return out

@@ -156,3 +156,10 @@ def channel_sample(cdf: np.ndarray, seed: int, offset: int, n: int, B: int,
     b = None if bits is None else np.ascontiguousarray(bits, dtype=np.uint8)
     lib().ibo_channel_sample(cdf, len(cdf) - 1, seed, offset, n * B, None if b is None else b.ctypes.data, out)
     return out
+
+
+def random_bits(seed: int, offset: int, n: int, B: int) -> np.ndarray:
+    """u8 [n][B] information bits of ibl_random_bits: top bit of each 64-bit output of numpy's
+    Philox4x64-10 stream with key seed, counter offset (the stand-in for LDPC_Transmitter.py:111's
+    np.random.randint(0, 2, (data_len, msg_at_time)))."""
+    return (philox_raw(int(offset), int(seed), int(n) * int(B)) >> np.uint64(63)).astype(np.uint8).reshape(n, B)

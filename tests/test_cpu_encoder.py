@@ -1,0 +1,109 @@
+"""CPU tests of the encoder oracle (oracle/encoder_oracle.py) against the reference's own encode
+(tests/golden/reference_encoder.npz, made by tests/golden/make_golden_encoder.py), plus the
+parity-check property on every plan shape the reference distinguishes (getLDPCEncoderParamters,
+Discrete_LDPC_decoding/LDPC_encoder.py:197-269)."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from informationbottleneckdecodingldpc_amd import codes
+from oracle import encoder_oracle as eo
+from oracle import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "reference_encoder.npz")
+_CODES = {"wlan": lambda: codes.wlan_80211n(54), "dvb": lambda: codes.dvbs2_structured(seed=0)}
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLD, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("name", ["wlan", "dvb"])
+def test_oracle_equals_reference_encode(gold, name):
+    H = _CODES[name]()
+    plan = eo.EncoderPlan(H)
+    assert plan.algo == str(gold[f"{name}_algo"])
+    ro = gold[f"{name}_roworder"]
+    if ro[0] >= 0:
+        np.testing.assert_array_equal(plan.row_order, ro)
+    else:
+        assert plan.row_order is None
+    Y = eo.encode(plan, gold[f"{name}_X"])
+    np.testing.assert_array_equal(Y, gold[f"{name}_Y"])
+
+
+def _syndrome(H, Y):
+    return (sp.csr_matrix(H).astype(np.int64) @ Y.astype(np.int64)) & 1
+
+
+def _with_parity(B_part, K=40, seed=1):
+    rng = np.random.default_rng(seed)
+    M = B_part.shape[0]
+    A = (rng.random((M, K)) < 0.1).astype(np.int8)
+    return sp.csr_matrix(np.hstack([A, B_part.astype(np.int8)]))
+
+
+def _tri(M, lower, seed):
+    rng = np.random.default_rng(seed)
+    T = (rng.random((M, M)) < 0.15).astype(np.int8)
+    T = np.tril(T, -1) if lower else np.triu(T, 1)
+    return T + np.eye(M, dtype=np.int8)
+
+
+@pytest.mark.parametrize("kind,algo", [
+    ("lower", "Forward Substitution"), ("upper", "Backward Substitution"),
+    ("rev_lower", "Forward Substitution"), ("rev_upper", "Backward Substitution"),
+    ("bidiag", "Forward Substitution"), ("dense", "Matrix Inverse")])
+def test_plan_shapes_give_codewords(kind, algo):
+    M = 30
+    if kind in ("lower", "upper"):
+        Bp = _tri(M, kind == "lower", 3)
+    elif kind.startswith("rev_"):
+        Bp = _tri(M, kind == "rev_lower", 4)[::-1]
+    elif kind == "bidiag":
+        Bp = np.eye(M, dtype=np.int8) + np.eye(M, k=-1, dtype=np.int8)
+    else:
+        rng = np.random.default_rng(5)
+        while True:   # a GF(2)-invertible, non-triangular parity part
+            Bp = (rng.random((M, M)) < 0.3).astype(np.int8)
+            _, _, _, ok = eo.gf2factorize(Bp)
+            if ok and eo._is_full_diag_triangular(sp.csr_matrix(Bp)) == 0:
+                break
+    H = _with_parity(Bp)
+    plan = eo.EncoderPlan(H)
+    assert plan.algo == algo
+    X = np.random.default_rng(6).integers(0, 2, (H.shape[1] - M, 7)).astype(np.uint8)
+    Y = eo.encode(plan, X)
+    np.testing.assert_array_equal(Y[: X.shape[0]], X)
+    assert not _syndrome(H, Y).any()
+
+
+def test_singular_parity_part_raises():
+    M = 10
+    Bp = np.eye(M, dtype=np.int8)
+    Bp[3] = Bp[4]                       # duplicate row -> singular, not triangular
+    Bp[3, 7] = 1
+    Bp[4, 7] = 1
+    with pytest.raises(ValueError):
+        eo.EncoderPlan(_with_parity(Bp))
+
+
+def test_wlan_n1944_and_single_word():
+    H = codes.wlan_80211n(81)
+    plan = eo.EncoderPlan(H)
+    X = np.random.default_rng(7).integers(0, 2, (H.shape[1] - H.shape[0], 5)).astype(np.uint8)
+    Y = eo.encode(plan, X)
+    assert not _syndrome(H, Y).any()
+    np.testing.assert_array_equal(eo.encode(plan, X[:, 2]), Y[:, 2])
+
+
+@pytest.mark.parametrize("seed,offset,n,B", [(0, 0, 5, 3), (11, 7, 33, 9), (2 ** 40 + 3, 2 ** 33, 8, 4)])
+def test_random_bits_are_top_bits_of_numpy_philox(seed, offset, n, B):
+    g = np.random.Philox(key=seed)
+    g.advance(offset)
+    ref = (g.random_raw(n * B) >> np.uint64(63)).astype(np.uint8).reshape(n, B)
+    np.testing.assert_array_equal(oracle.random_bits(seed, offset, n, B), ref)

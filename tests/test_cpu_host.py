@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(L, s), s
     assert sorted(lib.EXPORTS) == syms
-    assert L.ibl_version() == 2
+    assert L.ibl_version() == 3
 
 
 def test_library_device_count_without_gpu(lib):
