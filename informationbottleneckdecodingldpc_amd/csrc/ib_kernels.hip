@@ -76,8 +76,9 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
 // each row (W = rowW<MAXD>()), a wave item = one node x 512*W codewords (256*W-B row segments).
 __device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
 
-__device__ __forceinline__ uint32_t valid_mask8(int remaining) {
-  return remaining >= 8 ? 0xFFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
+// all-ones nibbles for the codewords of a word that lie inside the batch
+__device__ __forceinline__ uint32_t valid_nib8(int remaining) {
+  return remaining >= 8 ? 0xFFFFFFFFu : (remaining <= 0 ? 0u : ((1u << (4 * remaining)) - 1u));
 }
 
 template <int W> struct RowVec;
@@ -212,17 +213,18 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
   }
   const uint32_t fbase = slot_off(fslot);
   if (do_par) {
+    // Syndrome of all 8 codewords of a word at once (calc_syndrome, kernels_template_irreg.cl:
+    // 304-326: parity of (m < T/2) over the check's inputs). Adding 8 - T/2 to every nibble sets
+    // its bit 3 iff m >= T/2 without a carry into the next nibble (m < T <= 16), so the XOR of the
+    // D biased words holds in bit 3 of nibble k the parity of (m >= T/2) of codeword k; the parity
+    // of (m < T/2) is that XOR (D & 1).
+    const uint32_t bias = (uint32_t)(8 - a.half) * 0x11111111u;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
-      uint32_t par = 0;
+      uint32_t x = (D & 1) ? 0x88888888u : 0u;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        uint32_t p = 0;
-#pragma unroll
-        for (int j = 0; j < D; ++j) p ^= (nib(b.row[j][i], k) < (uint32_t)a.half) ? 1u : 0u;
-        par |= p << k;
-      }
-      if (par & valid_mask8(a.B - b.cwb - 8 * i)) unsat = true;
+      for (int j = 0; j < D; ++j) x ^= b.row[j][i] + bias;
+      if (x & 0x88888888u & valid_nib8(a.B - b.cwb - 8 * i)) unsat = true;
     }
   }
 #pragma unroll
