@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default=None,
                    help="BASELINE.json config preset (sets --code/--kind/--imax/--batch-per-gpu)")
     p.add_argument("--no-match", action="store_true")
+    p.add_argument("--float-path", choices=["auto", "passes", "fused"], default="auto",
+                   help="float decoders: fused on-chip kernel when the code fits in LDS (auto), or per-pass launches")
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -124,7 +126,7 @@ def main():
         w, dtype = 1, "u8"
     else:
         kind = 0 if a.kind == "minsum" else 1
-        dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32)
+        dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.float_path)
         cl = q.sample_all_zero_device(n_v, B, dev, generator=gen, dtype=torch.int64)
         llr = torch.as_tensor(q.output_LLRs, dtype=torch.float32, device=dev)[cl].contiguous()
         out = torch.empty((n_v, B), dtype=torch.float32, device=dev)
@@ -173,7 +175,13 @@ def main():
     # bytes actually stored by this build: the IB fast path keeps 4-bit messages/channel values
     ws = 0.5 if (a.kind == "ib" and getattr(dec, "fast_path", False)) else w
     fmt = {0.5: "u4", 1: "u8", 4: "f32"}[ws]
-    if vn_ms >= cn_ms:
+    fused = a.kind != "ib" and dec.fused
+    if fused:
+        # one fl_fused launch decodes the batch with the messages in LDS: its algorithmic bytes are the
+        # whole decode's (SURVEY §8(d) per codeword x B); HBM moves only channel in + APP out
+        kname, kavg, kbytes, kstored = "fl_fused", cn_avg, bpc * B, 2 * n_v * w * B
+        fmt = "f32 (messages in LDS)"
+    elif vn_ms >= cn_ms:
         kname, kavg, kbytes, kstored = ("ib_vn_fast" if a.kind == "ib" else "fl_vn"), vn_avg, vn_bytes, int(vn_bytes * ws / w)
     else:
         kname, kavg, kbytes, kstored = ("ib_cn_fast" if a.kind == "ib" else "fl_cn"), cn_avg, cn_bytes, int(cn_bytes * ws / w)
@@ -257,7 +265,9 @@ def main():
                     f"{'random T=16 IB tables' if a.kind == 'ib' else 'cluster LLRs'}; {code_desc}",
             "config": {"workload": f"{code_name}, "
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
-                                   f"{B} codewords per GPU, matching {'on' if match else 'off'}, fixed iterations",
+                                   f"{B} codewords per GPU, "
+                                   f"{('matching ' + ('on' if match else 'off')) if a.kind == 'ib' else ('fused on-chip kernel' if fused else 'per-pass kernels')}"
+                                   f", fixed iterations",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
             "hbm_gbps_algorithmic": round(value * bpc / 1e9, 1),
@@ -273,7 +283,11 @@ def main():
                                   "messages, so the HBM bytes actually moved are achieved_stored/frac_stored "
                                   "(a u8-equivalent frac above 1 is the nibble format beating the u8 roofline); "
                                   "the kernel is bound by LDS lookups + VALU issue, see lds_lookups_per_clk_per_cu")
-                         if fmt == "u4" else None,
+                         if fmt == "u4" else
+                         ("fused on-chip decoder: every message of a workgroup's codewords stays in LDS for all "
+                          "iterations, so achieved/frac price the algorithmic (HBM-resident design) bytes the kernel "
+                          "avoids; it is bound by LDS/VALU issue, and the HBM bytes it moves are achieved_stored")
+                         if fused else None,
                          "launches": {"cn": cn_n, "vn": vn_n},
                          "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}},
             "cpu_baseline": cpu,

@@ -32,6 +32,7 @@ extern "C" {
 enum { IBL_OK = 0, IBL_EINVAL = -1, IBL_EHIP = -2, IBL_ENOMEM = -3, IBL_EUNSUPPORTED = -4 };
 enum { IBL_U8 = 1, IBL_I32 = 2, IBL_F32 = 3, IBL_F64 = 4 };
 enum { IBL_MINSUM = 0, IBL_BP = 1 };
+enum { IBL_PATH_AUTO = 0, IBL_PATH_PASSES = 1, IBL_PATH_FUSED = 2 };
 enum { IBL_FLAG_FORCE_GENERIC = 1 };
 
 typedef struct ibl_graph ibl_graph;
@@ -124,6 +125,17 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
 int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out,
                      int32_t out_dtype, int32_t early_stop, int32_t* d_iters, void* stream);
 void ibl_float_destroy(ibl_float* h);
+/*
+ * Decode path of a float decoder (no reference counterpart; results are identical on both):
+ *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits in LDS
+ *                            ((E + N) * 16 bytes <= 160 KiB, check degrees >= 2), else IBL_PATH_PASSES;
+ *   IBL_PATH_PASSES          one launch per check / variable pass, messages in HBM;
+ *   IBL_PATH_FUSED           the fused kernel (IBL_EUNSUPPORTED if the code does not fit).
+ * ibl_float_path_in_use reports 1 when decodes run the fused kernel, 0 otherwise.  With the fused
+ * kernel the timing API reports each fused launch as one check-node launch (vn counts stay 0).
+ */
+int ibl_float_set_path(ibl_float* h, int32_t path);
+int ibl_float_path_in_use(const ibl_float* h, int32_t* fused);
 int ibl_float_timing(ibl_float* h, int32_t enable);
 int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_launches, double* vn_ms, int32_t* vn_launches);
 

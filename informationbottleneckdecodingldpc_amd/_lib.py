@@ -20,6 +20,7 @@ IBL_OK, IBL_EINVAL, IBL_EHIP, IBL_ENOMEM, IBL_EUNSUPPORTED = 0, -1, -2, -3, -4
 IBL_U8, IBL_I32, IBL_F32, IBL_F64 = 1, 2, 3, 4
 IBL_MINSUM, IBL_BP = 0, 1
 IBL_FLAG_FORCE_GENERIC = 1
+IBL_PATH_AUTO, IBL_PATH_PASSES, IBL_PATH_FUSED = 0, 1, 2
 
 # every symbol declared in include/ibldpc.h
 EXPORTS = [
@@ -27,6 +28,7 @@ EXPORTS = [
     "ibl_graph_create", "ibl_graph_info", "ibl_graph_destroy",
     "ibl_ib_create", "ibl_ib_path", "ibl_ib_decode", "ibl_ib_destroy",
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
+    "ibl_float_set_path", "ibl_float_path_in_use",
     "ibl_ib_timing", "ibl_ib_timing_read", "ibl_float_timing", "ibl_float_timing_read",
     "ibl_channel_sample",
     "ibl_encoder_create",
@@ -76,6 +78,8 @@ def load():
     L.ibl_float_decode.argtypes = [_vp, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]
     L.ibl_float_destroy.argtypes = [_vp]
     L.ibl_float_destroy.restype = None
+    L.ibl_float_set_path.argtypes = [_vp, _i32]
+    L.ibl_float_path_in_use.argtypes = [_vp, ctypes.POINTER(_i32)]
     for nm in ("ibl_ib_timing", "ibl_float_timing"):
         getattr(L, nm).argtypes = [_vp, _i32]
     for nm in ("ibl_ib_timing_read", "ibl_float_timing_read"):

@@ -173,6 +173,13 @@ struct ibl_float {
   int32_t *flags = nullptr, *dL = nullptr;
   int grid_cn = 0, grid_vn = 0;
   KTimer timer;
+  // fused on-chip path (FlFusedArgs): task tables, LDS bytes per workgroup, grid
+  int32_t path = IBL_PATH_AUTO;
+  bool fused_ok = false;
+  int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
+  int32_t f_ncn = 0, f_nvn = 0, f_maxd = 0;
+  size_t f_lds = 0;
+  int f_grid = 0;
 };
 
 extern "C" {
@@ -605,6 +612,108 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
 }
 
 // ------------------------------------------------------------------ float decoder
+}  // extern "C"
+
+namespace {
+// Task tables of the fused float kernel (FlFusedArgs). Check nodes sorted by degree (heaviest first,
+// stable) and cut into tasks of up to 64 nodes of one degree; edge k of lane i of a check task gets
+// slot first + k*count + i. Variable nodes likewise; vn_slot maps each variable edge (task-major,
+// k*count + i) to the slot of the same edge. Leaves fused_ok false when the code does not fit.
+int fused_setup(ibl_float* h) {
+  const ibl_graph* g = h->g;
+  const int64_t E = g->n_e;
+  const size_t lds = (size_t)(E + g->n_v) * 16 + 16;
+  int min_dc = 1 << 30;
+  for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
+  if (lds > (size_t)kLdsBytes || min_dc < 2 || E == 0) return IBL_OK;
+  const int maxd = std::max(g->dcm, g->dvm);
+  int bpc = 0, block = 0;
+  if (fl_fused_occupancy(h->kind, h->prec, maxd, lds, &bpc, &block) != hipSuccess || bpc < 1) {
+    (void)hipGetLastError();
+    return IBL_OK;
+  }
+  std::vector<int32_t> tgt_vn((size_t)E);
+  if (hipMemcpy(tgt_vn.data(), g->tgt_vn, sizeof(int32_t) * (size_t)E, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(IBL_EHIP, "hipMemcpy failed");
+  auto starts = [](const std::vector<int32_t>& deg) {
+    std::vector<int64_t> st(deg.size() + 1, 0);
+    for (size_t i = 0; i < deg.size(); ++i) st[i + 1] = st[i] + deg[i];
+    return st;
+  };
+  auto sorted = [](const std::vector<int32_t>& deg) {
+    std::vector<int32_t> idx(deg.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
+    return idx;
+  };
+  const std::vector<int64_t> cst = starts(g->h_cn_deg), vst = starts(g->h_vn_deg);
+  std::vector<int32_t> slot_of((size_t)E), cn_task, vn_task, vn_node, vn_slot;
+  {
+    const std::vector<int32_t> ord = sorted(g->h_cn_deg);
+    int32_t slot = 0;
+    for (size_t i = 0; i < ord.size();) {
+      const int32_t d = g->h_cn_deg[ord[i]];
+      int32_t cnt = 0;
+      while (i + cnt < ord.size() && cnt < 64 && g->h_cn_deg[ord[i + cnt]] == d) ++cnt;
+      cn_task.insert(cn_task.end(), {slot, cnt, d, 0});
+      for (int32_t l = 0; l < cnt; ++l)
+        for (int32_t k = 0; k < d; ++k) slot_of[(size_t)cst[ord[i + l]] + k] = slot + k * cnt + l;
+      slot += cnt * d;
+      i += cnt;
+    }
+  }
+  {
+    const std::vector<int32_t> ord = sorted(g->h_vn_deg);
+    int32_t sidx = 0;
+    for (size_t i = 0; i < ord.size();) {
+      const int32_t d = g->h_vn_deg[ord[i]];
+      int32_t cnt = 0;
+      while (i + cnt < ord.size() && cnt < 64 && g->h_vn_deg[ord[i + cnt]] == d) ++cnt;
+      vn_task.insert(vn_task.end(), {(int32_t)i, cnt, d, sidx});
+      vn_slot.resize((size_t)sidx + (size_t)cnt * d);
+      for (int32_t l = 0; l < cnt; ++l) {
+        const int32_t v = ord[i + l];
+        vn_node.push_back(v);
+        for (int32_t k = 0; k < d; ++k) vn_slot[(size_t)sidx + k * cnt + l] = slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]];
+      }
+      sidx += cnt * d;
+      i += cnt;
+    }
+  }
+  int rc;
+  if ((rc = dupload(&h->f_cn_task, cn_task.data(), cn_task.size())) ||
+      (rc = dupload(&h->f_vn_task, vn_task.data(), vn_task.size())) ||
+      (rc = dupload(&h->f_vn_node, vn_node.data(), vn_node.size())) ||
+      (rc = dupload(&h->f_vn_slot, vn_slot.data(), vn_slot.size())))
+    return rc;
+  h->f_ncn = (int32_t)(cn_task.size() / 4);
+  h->f_nvn = (int32_t)(vn_task.size() / 4);
+  h->f_maxd = maxd;
+  h->f_lds = lds;
+  h->f_grid = bpc * g->num_cus;
+  h->fused_ok = true;
+  return IBL_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ibl_float_set_path(ibl_float* h, int32_t path) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (path != IBL_PATH_AUTO && path != IBL_PATH_PASSES && path != IBL_PATH_FUSED)
+    return fail(IBL_EINVAL, "path must be IBL_PATH_AUTO, IBL_PATH_PASSES or IBL_PATH_FUSED");
+  if (path == IBL_PATH_FUSED && !h->fused_ok)
+    return fail(IBL_EUNSUPPORTED, "code does not fit the fused kernel ((E + N) * 16 B > 160 KiB or a check degree < 2)");
+  h->path = path;
+  return IBL_OK;
+}
+
+int ibl_float_path_in_use(const ibl_float* h, int32_t* fused) {
+  if (!h || !fused) return fail(IBL_EINVAL, "NULL argument");
+  *fused = (h->fused_ok && h->path != IBL_PATH_PASSES) ? 1 : 0;
+  return IBL_OK;
+}
+
 int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_max, int32_t precision,
                      int32_t max_batch, ibl_float** out) {
   if (!out) return fail(IBL_EINVAL, "out is NULL");
@@ -639,6 +748,7 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   h->grid_cn = std::min(bpc, 1024 / fl_block(0, kind, precision, g->dcm)) * g->num_cus;
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_vn = std::min(bpc, 1024 / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
+  if ((rc = fused_setup(h))) return bail(rc);
   *out = h;
   return IBL_OK;
 }
@@ -647,6 +757,7 @@ void ibl_float_destroy(ibl_float* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
+  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
   delete h;
 }
 
@@ -666,6 +777,25 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   const int nchunks = (B + 64 * cwl - 1) / (64 * cwl);
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
   HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, s));
+  if (h->fused_ok && h->path != IBL_PATH_PASSES) {
+    FlFusedArgs fa{};
+    fa.ch = h->chf; fa.cn_task = h->f_cn_task; fa.vn_task = h->f_vn_task; fa.vn_node = h->f_vn_node;
+    fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
+    fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
+    fa.n_vn_tasks = h->f_nvn; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
+    fa.ngroups = (B + cwl - 1) / cwl;
+    const size_t esz = out_dtype == kF32 ? 4 : 8;
+    fa.aligned = ((B % cwl) == 0 && ((uintptr_t)d_out % (cwl * esz)) == 0) ? 1 : 0;
+    const int grid = std::min(fa.ngroups, h->f_grid);
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, h->f_maxd, grid, h->f_lds, s); }));
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    if (early) {   // batch-global stop before imax-1: re-run the batch to L (the kernel exits if L = imax-1)
+      fa.unsat = nullptr;
+      fa.dL = h->dL;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, h->f_maxd, grid, h->f_lds, s); }));
+    }
+    return IBL_OK;
+  }
   FlArgs send{};
   send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
   send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;

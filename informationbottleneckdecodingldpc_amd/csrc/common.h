@@ -125,6 +125,23 @@ struct FlArgs {
   int32_t n_nodes, nchunks, ldb, B;
 };
 
+// Fused float decoder: a workgroup keeps Vec<F>::N codewords (one 16-byte slot per edge) entirely
+// in LDS for all iterations. Edge slots are numbered per check-node task (up to 64 check nodes of
+// one degree, lane = node): edge k of lane i of a task at slot first + k*count + i, so the check
+// pass reads and writes contiguous 16-byte slots; the variable pass gathers through vn_slot.
+struct FlFusedArgs {
+  const void* ch;           // staged channel LLRs [N][ldb] (F)
+  const int32_t* cn_task;   // per check task: {first slot, count, degree, 0}
+  const int32_t* vn_task;   // per variable task: {first position, count, degree, first vn_slot index}
+  const int32_t* vn_node;   // variable position -> node
+  const int32_t* vn_slot;   // variable task edge k, lane i at [first + k*count + i] -> message slot
+  void* out;                // user output [N][B] (out_dtype)
+  int32_t* unsat;           // non-null: CN pass j ORs "unsatisfied" into unsat[(j-1)*kShards + shard]
+  const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
+  double llr_max;
+  int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, ldb, B, imax, out_dtype, aligned, ngroups;
+};
+
 struct FlDecArgs {
   const void* vin0;         // ping-pong varnode inboxes, selected by parity of L
   const void* vin1;
@@ -187,5 +204,7 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
 int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
+hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s);
+hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block);
 
 }  // namespace ibl

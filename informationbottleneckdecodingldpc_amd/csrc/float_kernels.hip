@@ -111,33 +111,11 @@ struct FlOut {
   }
 };
 
-template <int KIND, typename F, int D>
-__device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, bool do_par, int valid, bool& unsat) {
-  using V = Vec<F>;
-  constexpr int N = V::N;
-  const F* src = reinterpret_cast<const F*>(a.in);
-  const F lm = (F)a.llr_max;
-  int tg[D];   // output rows, loaded up front as scalars (the stores follow each output)
-#pragma unroll
-  for (int w = 0; w < D; ++w) tg[w] = sload(a.tgt, st + w);
-  F m[D][N];
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const typename V::T r = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
-#pragma unroll
-    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
-  }
-  if (do_par) {
-#pragma unroll
-    for (int s = 0; s < N; ++s) {
-      bool p = false;
-#pragma unroll
-      for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
-      unsat |= p && s < valid;
-    }
-  }
+// Check-node body on the inputs m (min-sum or BP); put(w, o) receives output w (any order of w).
+template <int KIND, typename F, int D, class Put>
+__device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put&& put) {
+  constexpr int N = Vec<F>::N;
   F o[N];
-  FlOut<F, D> ob;
   if constexpr (KIND == 0) {
     // min-sum (kernels_min_and_BP.cl:156-162): |out_w| = min over the others, sign = product
     F mn1[N], mn2[N];
@@ -163,7 +141,7 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
         const bool ng = neg[s] ^ (m[w][s] < F(0));
         o[s] = (nz[s] - (zw ? 1 : 0)) > 0 ? F(0) : (ng ? -mag : mag);
       }
-      ob.put(a, tg, cw0, w, o);
+      put(w, o);
     }
   } else {
     // BP sequential box-plus folds with prefix sharing (kernels_min_and_BP.cl:63-69)
@@ -176,7 +154,7 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
       for (int s = 0; s < N; ++s) t[s] = boxplus(m[j][s], t[s], lm);
 #pragma unroll
     for (int s = 0; s < N; ++s) o[s] = clampllr(t[s], lm);
-    ob.put(a, tg, cw0, 0, o);
+    put(0, o);
 #pragma unroll
     for (int s = 0; s < N; ++s) P[s] = m[0][s];
 #pragma unroll
@@ -189,19 +167,19 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
         for (int s = 0; s < N; ++s) t[s] = boxplus(m[j][s], t[s], lm);
 #pragma unroll
       for (int s = 0; s < N; ++s) o[s] = clampllr(t[s], lm);
-      ob.put(a, tg, cw0, w, o);
+      put(w, o);
 #pragma unroll
       for (int s = 0; s < N; ++s) P[s] = boxplus(m[w][s], P[s], lm);
     }
 #pragma unroll
     for (int s = 0; s < N; ++s) o[s] = clampllr(P[s], lm);
-    ob.put(a, tg, cw0, D - 1, o);
+    put(D - 1, o);
   }
-  ob.flush(a, tg, cw0);
 }
 
-template <typename F, int D>
-__device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, int cw0) {
+
+template <int KIND, typename F, int D>
+__device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, bool do_par, int valid, bool& unsat) {
   using V = Vec<F>;
   constexpr int N = V::N;
   const F* src = reinterpret_cast<const F*>(a.in);
@@ -209,23 +187,36 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
   int tg[D];   // output rows, loaded up front as scalars (the stores follow each output)
 #pragma unroll
   for (int w = 0; w < D; ++w) tg[w] = sload(a.tgt, st + w);
-  F c[N], m[D][N], o[N];
-  FlOut<F, D> ob;
-  {
-    const typename V::T r = *reinterpret_cast<const typename V::T*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
-#pragma unroll
-    for (int s = 0; s < N; ++s) c[s] = V::get(r, s);
-  }
+  F m[D][N];
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     const typename V::T r = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
 #pragma unroll
     for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
   }
+  if (do_par) {
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      bool p = false;
+#pragma unroll
+      for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
+      unsat |= p && s < valid;
+    }
+  }
+  FlOut<F, D> ob;
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(a, tg, cw0, w, o); });
+  ob.flush(a, tg, cw0);
+}
+
+// Variable-node body on channel c and inputs m; put(w, o) receives extrinsic output w.
+template <typename F, int D, class Put>
+__device__ __forceinline__ void fl_vn_body(const F (&c)[Vec<F>::N], const F (&m)[D][Vec<F>::N], F lm, Put&& put) {
+  constexpr int N = Vec<F>::N;
+  F o[N];
   if constexpr (D == 1) {
 #pragma unroll
     for (int s = 0; s < N; ++s) o[s] = clampllr(c[s], lm);
-    ob.put(a, tg, cw0, 0, o);
+    put(0, o);
   } else {
     // t = ch + others in ascending order (kernels_min_and_BP.cl:113-118)
     F t[N], Q[N];
@@ -237,7 +228,7 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
       for (int s = 0; s < N; ++s) t[s] = t[s] + m[j][s];
 #pragma unroll
     for (int s = 0; s < N; ++s) o[s] = clampllr(t[s], lm);
-    ob.put(a, tg, cw0, 0, o);
+    put(0, o);
 #pragma unroll
     for (int s = 0; s < N; ++s) Q[s] = c[s] + m[0][s];
 #pragma unroll
@@ -250,14 +241,40 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
         for (int s = 0; s < N; ++s) t[s] = t[s] + m[j][s];
 #pragma unroll
       for (int s = 0; s < N; ++s) o[s] = clampllr(t[s], lm);
-      ob.put(a, tg, cw0, w, o);
+      put(w, o);
 #pragma unroll
       for (int s = 0; s < N; ++s) Q[s] = Q[s] + m[w][s];
     }
 #pragma unroll
     for (int s = 0; s < N; ++s) o[s] = clampllr(Q[s], lm);
-    ob.put(a, tg, cw0, D - 1, o);
+    put(D - 1, o);
   }
+}
+
+
+template <typename F, int D>
+__device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, int cw0) {
+  using V = Vec<F>;
+  constexpr int N = V::N;
+  const F* src = reinterpret_cast<const F*>(a.in);
+  const F lm = (F)a.llr_max;
+  int tg[D];   // output rows, loaded up front as scalars (the stores follow each output)
+#pragma unroll
+  for (int w = 0; w < D; ++w) tg[w] = sload(a.tgt, st + w);
+  F c[N], m[D][N];
+  {
+    const typename V::T r = *reinterpret_cast<const typename V::T*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
+#pragma unroll
+    for (int s = 0; s < N; ++s) c[s] = V::get(r, s);
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const typename V::T r = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
+#pragma unroll
+    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
+  }
+  FlOut<F, D> ob;
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(a, tg, cw0, w, o); });
   ob.flush(a, tg, cw0);
 }
 
@@ -431,6 +448,202 @@ __global__ void fl_send(FlArgs a) {
   }
 }
 
+// ------------------------------------------------------------ fused on-chip decoder
+// For codes whose messages fit in LDS ((E + N) * 16 B <= 160 KiB, e.g. WLAN N=1944: 142.6 KB), one
+// workgroup decodes Vec<F>::N codewords (4 fp32 / 2 fp64, one 16-byte slot per edge and per
+// variable) through ALL iterations without touching HBM: the flooding schedule of
+// decode_OpenCL_min_sum / decode_OpenCL_belief_propagation (min_sum_decoder_irreg.py:221-287,
+// bp_decoder_irreg.py:221-286) as barrier-separated phases over one in-place message array:
+//   send (kernels_min_and_BP.cl:12-29); for j = 1..L { CN pass (+ syndrome of its inputs, :206-227);
+//   VN pass (:76-123) unless j == L }; APP output (:170-204) from the last CN pass.
+// Check and variable nodes own their slots (a node reads all its inputs before writing its outputs
+// to the same slots), so one array serves both directions. Node bodies are the per-pass kernels'
+// (fl_cn_body / fl_vn_body), same operations in the same order: outputs equal the per-pass path's
+// bit for bit. Work inside a phase: tasks of up to 64 same-degree nodes, heaviest first, handed to
+// waves by LDS tickets; two counters alternate between phases (reset one phase ahead).
+// Early stop is batch-global in the reference (stop when the WHOLE batch's syndrome is zero): pass 1
+// runs imax-1 iterations and records each CN pass's syndrome in the same flag words as the per-pass
+// path; finalize_iters turns them into L; pass 2 (dL set) re-runs the batch to L only if L < imax-1.
+template <typename F>
+__device__ __forceinline__ typename Vec<F>::T fl_pack(const F (&o)[Vec<F>::N]) {
+  typename Vec<F>::T v;
+#pragma unroll
+  for (int s = 0; s < Vec<F>::N; ++s) Vec<F>::set(v, s, o[s]);
+  return v;
+}
+
+template <int KIND, typename F, int D>
+__device__ __forceinline__ void fused_cn_item(typename Vec<F>::T* msg, int first, int cnt, int lane, F lm,
+                                              bool do_par, int valid, bool& unsat) {
+  using V = Vec<F>;
+  constexpr int N = V::N;
+  F m[D][N];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const typename V::T r = msg[first + j * cnt + lane];
+#pragma unroll
+    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
+  }
+  if (do_par) {
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      bool p = false;
+#pragma unroll
+      for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
+      unsat |= p && s < valid;
+    }
+  }
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+    msg[first + w * cnt + lane] = fl_pack<F>(o);
+  });
+}
+
+template <typename F, int D>
+__device__ __forceinline__ void fused_vn_item(typename Vec<F>::T* msg, const typename Vec<F>::T* chL,
+                                              const int32_t* vn_slot, int pos, int sfirst, int cnt, int lane, F lm) {
+  using V = Vec<F>;
+  constexpr int N = V::N;
+  int sl[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) sl[k] = vn_slot[sfirst + k * cnt + lane];
+  F c[N], m[D][N];
+  {
+    const typename V::T r = chL[pos];
+#pragma unroll
+    for (int s = 0; s < N; ++s) c[s] = V::get(r, s);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const typename V::T r = msg[sl[k]];
+#pragma unroll
+    for (int s = 0; s < N; ++s) m[k][s] = V::get(r, s);
+  }
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { msg[sl[w]] = fl_pack<F>(o); });
+}
+
+template <int KIND, typename F, int MAXD>
+__global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(FlFusedArgs a) {
+  using V = Vec<F>;
+  using VT = typename V::T;
+  constexpr int N = V::N;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  VT* msg = reinterpret_cast<VT*>(lds);
+  VT* chL = msg + a.n_e;
+  int* ctr = reinterpret_cast<int*>(chL + a.n_v);
+  const int lane = threadIdx.x & 63;
+  const F lm = (F)a.llr_max;
+  int L = a.imax - 1;
+  if (a.dL) {
+    L = __builtin_amdgcn_readfirstlane(*a.dL);
+    if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
+  }
+  if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+  __syncthreads();
+  int ph = 0;
+  const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
+  // one phase: tasks dealt by ticket; the next phase's counter is reset while this one runs
+  auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
+    int* c = ctr + (ph & 1);
+    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    for (;;) {
+      const int t = take_ticket(c, lane);
+      if (t >= ntasks) break;
+      body(t);
+    }
+    __syncthreads();
+    ++ph;
+  };
+  for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+    const int cw0 = grp * N;
+    const int valid = a.B - cw0;
+    // send: every variable's channel slot and its edge slots
+    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
+      const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+      const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+      if (lane < cnt) {
+        const int node = a.vn_node[pos + lane];
+        const VT c = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
+        chL[pos + lane] = c;
+        for (int k = 0; k < d; ++k) msg[a.vn_slot[sf + k * cnt + lane]] = c;
+      }
+    });
+    for (int j = 1; j <= L; ++j) {
+      const bool do_par = a.unsat != nullptr;
+      bool unsat = false;
+      phase(a.n_cn_tasks, [&](int t) __attribute__((always_inline)) {
+        const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
+        if (lane < cnt) {
+          switch (d) {
+#define X(D) case D: if constexpr (D <= MAXD) fused_cn_item<KIND, F, D>(msg, first, cnt, lane, lm, do_par, valid, unsat); break;
+            FL_DEG_CASES(X)
+#undef X
+            default: break;
+          }
+        }
+      });
+      if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
+      if (j == L) break;
+      phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
+        const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+        const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+        if (lane < cnt) {
+          switch (d) {
+            case 1: fused_vn_item<F, 1>(msg, chL, a.vn_slot, pos + lane, sf, cnt, lane, lm); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_vn_item<F, D>(msg, chL, a.vn_slot, pos + lane, sf, cnt, lane, lm); break;
+            FL_DEG_CASES(X)
+#undef X
+            default: break;
+          }
+        }
+      });
+    }
+    // APP output: ch + all inputs of the last CN pass in ascending edge order, unclamped
+    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
+      const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+      const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+      if (lane < cnt) {
+        const int node = a.vn_node[pos + lane];
+        F x[N];
+        {
+          const VT r = chL[pos + lane];
+#pragma unroll
+          for (int s = 0; s < N; ++s) x[s] = V::get(r, s);
+        }
+        if (L > 0)
+          for (int k = 0; k < d; ++k) {
+            const VT r = msg[a.vn_slot[sf + k * cnt + lane]];
+#pragma unroll
+            for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
+          }
+        const size_t o = (size_t)node * a.B + cw0;
+        if (a.out_dtype == kF32) {
+          float* p = reinterpret_cast<float*>(a.out) + o;
+          if constexpr (N == 4) {
+            if (a.aligned && valid >= 4) {
+              *reinterpret_cast<float4*>(p) = make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
+              return;
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < N; ++s)
+            if (s < valid) p[s] = (float)x[s];
+        } else {
+          double* p = reinterpret_cast<double*>(a.out) + o;
+          if constexpr (N == 2) {
+            if (a.aligned && valid >= 2) {
+              *reinterpret_cast<double2*>(p) = make_double2((double)x[0], (double)x[1]);
+              return;
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < N; ++s)
+            if (s < valid) p[s] = (double)x[s];
+        }
+      }
+    });
+  }
+}
+
 // ---------------------------------------------------------------------- launchers
 hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s) {
   const size_t total = (size_t)n * ldb;
@@ -476,6 +689,29 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
   FlArgs args = a;
   void* p[] = {&args};
   return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(fl_block(1, 0, prec, maxd)), p, 0, s);
+}
+
+static const void* fl_fused_kernel(int kind, int prec, int maxd) {
+  const bool f32 = prec == kF32, small = maxd <= 8;
+  if (kind == 0)
+    return f32 ? (small ? (const void*)fl_fused<0, float, 8> : (const void*)fl_fused<0, float, 16>)
+               : (small ? (const void*)fl_fused<0, double, 8> : (const void*)fl_fused<0, double, 16>);
+  return f32 ? (small ? (const void*)fl_fused<1, float, 8> : (const void*)fl_fused<1, float, 16>)
+             : (small ? (const void*)fl_fused<1, double, 8> : (const void*)fl_fused<1, double, 16>);
+}
+
+hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block) {
+  const void* f = fl_fused_kernel(kind, prec, maxd);
+  *block = fl_block(0, kind, prec, maxd);
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
+}
+
+hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s) {
+  FlFusedArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_fused_kernel(kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd)), p, lds, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {

@@ -131,10 +131,16 @@ class IBDecoder:
 
 
 class FloatDecoder:
-    """Float min-sum (kind=0) / BP (kind=1) decoder (``ibl_float``); precision fp32 or fp64."""
+    """Float min-sum (kind=0) / BP (kind=1) decoder (``ibl_float``); precision fp32 or fp64.
+
+    ``path``: "auto" (the fused on-chip kernel when the code fits in LDS), "passes" (one launch per
+    check / variable pass) or "fused" (raises when the code does not fit); both give identical
+    results (``ibl_float_set_path``). ``fused`` tells which one decodes run."""
+
+    _PATHS = {"auto": _lib.IBL_PATH_AUTO, "passes": _lib.IBL_PATH_PASSES, "fused": _lib.IBL_PATH_FUSED}
 
     def __init__(self, graph: Graph, kind: int, imax: int, max_batch: int, precision=torch.float32,
-                 llr_max: float = 150.0):
+                 llr_max: float = 150.0, path: str = "auto"):
         self.graph = graph
         self.kind = int(kind)
         self.imax = int(imax)
@@ -146,6 +152,15 @@ class FloatDecoder:
                                                 _DT_FL[precision], self.max_batch, ctypes.byref(h)),
                    "ibl_float_create")
         self._h = h
+        if path not in self._PATHS:
+            raise ValueError(f"path must be one of {sorted(self._PATHS)}")
+        _lib.check(_lib.load().ibl_float_set_path(h, self._PATHS[path]), "ibl_float_set_path")
+
+    @property
+    def fused(self) -> bool:
+        f = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_float_path_in_use(self._h, ctypes.byref(f)), "ibl_float_path_in_use")
+        return bool(f.value)
 
     def decode(self, llr: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=None,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
