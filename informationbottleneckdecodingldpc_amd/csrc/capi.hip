@@ -158,6 +158,9 @@ struct ibl_ib {
   uint32_t *cn_img = nullptr, *vn_img = nullptr, *dec_img = nullptr;
   int cn_nt = 0, vn_nt = 0, dec_nt = 0;   // fast path: LDS table regions (4 tables each) per pass
   int32_t cn_fslot[kMaxD + 1] = {0}, vn_fslot[kMaxD + 1] = {0};
+  uint32_t *cn_cimg = nullptr, *vn_cimg = nullptr;   // column images per pass (ncs x 32 dwords)
+  int cn_ncs = 0, vn_ncs = 0;
+  int8_t cn_ccol[kMaxD + 1][4] = {{0}}, vn_ccol[kMaxD + 1][4] = {{0}};
   KCfg kcn, kvn, kdec;
   KTimer timer;
   // generic path
@@ -323,8 +326,25 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
   return d;
 }
 
-int pick_cfg(int which, int maxd, int nt, int num_cus, KCfg* k) {
-  k->lds = (size_t)regions_of(nt) * kRegion + 64;   // tables + the fast kernels' 2 work counters
+// LDS bytes of a fast CN / VN launch: table regions, column images, the 2 work counters
+size_t fast_lds(int nt, int ncs) { return (size_t)regions_of(nt) * kRegion + (size_t)ncs * kColImg + 64; }
+
+// One pass's column images (colf): per image slot, 16 columns m x {entries t = 0..7, t = 8..15} as nibbles
+void append_cols(std::vector<uint32_t>& img, const std::vector<Table>& tbs, const std::vector<int>& slots) {
+  for (int s : slots)
+    for (int m = 0; m < kTP; ++m) {
+      uint32_t lo = 0, hi = 0;
+      for (int t = 0; t < 8; ++t) {
+        lo |= (uint32_t)(tbs[s][t * kTP + m] & 15) << (4 * t);
+        hi |= (uint32_t)(tbs[s][(t + 8) * kTP + m] & 15) << (4 * t);
+      }
+      img.push_back(lo);
+      img.push_back(hi);
+    }
+}
+
+int pick_cfg(int which, int maxd, int nt, int ncs, int num_cus, KCfg* k) {
+  k->lds = fast_lds(nt, ncs);
   int best_waves = 0;
   // largest block first at equal occupancy: a CU's waves then share one work counter
   for (int block : {1024, 768, 640, 512, 384, 256}) {
@@ -397,12 +417,43 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     for (int d : vdeg) vn_nt += (d >= 2);
   }
   const int max_nt = (kLdsBytes / kRegion) * 4;
+  // table slot of each column-fetched input (cn_ncols / vn_ncols): raw fold table, or the degree's
+  // final (matching-composed) table; slots are numbered as in the pass images below
+  std::vector<int> ccol_slot, vcol_slot;   // column image index -> table slot
+  auto col_index = [](std::vector<int>& v, int s) {
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i] == s) return (int8_t)i;
+    v.push_back(s);
+    return (int8_t)(v.size() - 1);
+  };
+  {
+    int slot = cn_nraw;
+    for (int d : cdeg) {
+      const int fs = h->match ? slot++ : (d >= 3 ? d - 3 : 0);
+      for (int i = 0, nc = cn_ncols(d); i < nc; ++i) {
+        const int l = d - nc + i - 2;   // input j = d-nc+i meets table j-2 in every non-prefix chain
+        h->cn_ccol[d][i] = col_index(ccol_slot, l == d - 3 ? fs : l);
+      }
+    }
+    slot = vn_nraw;
+    for (int d : vdeg) {
+      if (d < 2) continue;
+      const int fs = h->match ? slot++ : d - 2;
+      for (int i = 0, nc = vn_ncols(d); i < nc; ++i) {
+        const int l = d - nc + i - 1;   // input j meets table j-1
+        h->vn_ccol[d][i] = col_index(vcol_slot, l == d - 2 ? fs : l);
+      }
+    }
+  }
+  h->cn_ncs = (int)ccol_slot.size();
+  h->vn_ncs = (int)vcol_slot.size();
+  const bool lds_ok = fast_lds(cn_nt, h->cn_ncs) <= (size_t)kLdsBytes && fast_lds(std::max(vn_nt, 1), h->vn_ncs) <= (size_t)kLdsBytes;
   h->fast = !(flags & IBL_FLAG_FORCE_GENERIC) && Tc == T && T <= kTP && deg_ok && cn_nt <= max_nt &&
-            vn_nt <= max_nt && VM <= max_nt && cn_nt > 0;
+            vn_nt <= max_nt && VM <= max_nt && cn_nt > 0 && lds_ok;
 
   if (h->fast) {
     // ---------------- CN images: pass p = 0 (iteration 0 ops) .. imax-1
-    std::vector<uint32_t> cimg, vimg, dimg;
+    std::vector<uint32_t> cimg, vimg, dimg, ccimg, vcimg;
     const int64_t T2 = (int64_t)T * T;
     auto cn_raw = [&](int p, int l, int t, int m) -> int {
       int64_t idx;
@@ -425,6 +476,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
         h->cn_fslot[d] = slot++;
       }
       append_pass(cimg, tbs, regions_of(cn_nt));
+      append_cols(ccimg, tbs, ccol_slot);
     }
     h->cn_nt = regions_of(cn_nt);
     // ---------------- VN images: pass k = 0 .. imax-2 (extrinsic), decision images k = 0 .. imax-1
@@ -448,6 +500,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
         h->vn_fslot[d] = slot++;
       }
       append_pass(vimg, tbs, regions_of(std::max(vn_nt, 1)));
+      append_cols(vcimg, tbs, vcol_slot);
     }
     h->vn_nt = regions_of(std::max(vn_nt, 1));
     for (int k = 0; k < imax; ++k) {
@@ -457,10 +510,12 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     }
     h->dec_nt = regions_of(VM);
     if ((rc = dupload(&h->cn_img, cimg.data(), cimg.size())) || (rc = dupload(&h->vn_img, vimg.data(), vimg.size())) ||
-        (rc = dupload(&h->dec_img, dimg.data(), dimg.size())))
+        (rc = dupload(&h->dec_img, dimg.data(), dimg.size())) ||
+        (rc = dupload(&h->cn_cimg, ccimg.data(), ccimg.size())) || (rc = dupload(&h->vn_cimg, vcimg.data(), vcimg.size())))
       return bail(rc);
-    if ((rc = pick_cfg(0, CM, 4 * h->cn_nt, g->num_cus, &h->kcn)) || (rc = pick_cfg(1, VM, 4 * h->vn_nt, g->num_cus, &h->kvn)) ||
-        (rc = pick_cfg(2, VM, 4 * h->dec_nt, g->num_cus, &h->kdec)))
+    if ((rc = pick_cfg(0, CM, 4 * h->cn_nt, h->cn_ncs, g->num_cus, &h->kcn)) ||
+        (rc = pick_cfg(1, VM, 4 * h->vn_nt, h->vn_ncs, g->num_cus, &h->kvn)) ||
+        (rc = pick_cfg(2, VM, 4 * h->dec_nt, 0, g->num_cus, &h->kdec)))
       return bail(rc);
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
@@ -499,7 +554,7 @@ void ibl_ib_destroy(ibl_ib* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
-  dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img);
+  dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img); dfree(h->cn_cimg); dfree(h->vn_cimg);
   dfree(h->cn_lut); dfree(h->vn_lut); dfree(h->mc); dfree(h->mv);
   delete h;
 }
@@ -536,8 +591,12 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     cn.nt = h->cn_nt; vn.nt = h->vn_nt;
     std::memcpy(cn.fslot, h->cn_fslot, sizeof(cn.fslot));
     std::memcpy(vn.fslot, h->vn_fslot, sizeof(vn.fslot));
+    std::memcpy(cn.ccol, h->cn_ccol, sizeof(cn.ccol));
+    std::memcpy(vn.ccol, h->vn_ccol, sizeof(vn.ccol));
+    cn.ncs = h->cn_ncs; vn.ncs = h->vn_ncs;
     // pass 0: send + checknode_update_iter0, inputs gathered from the staged channel rows
     cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
+    cn.cimg = h->cn_cimg;
     HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); }));
     cn.in = h->cin; cn.gather = nullptr;
     // diagnostics: IBL_TRACE_WAVES=<prefix> records {start, end, items|cu} of every wave of the middle
@@ -549,10 +608,12 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     for (int j = 1; j < I; ++j) {
       const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
       vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
+      vn.cimg = h->vn_cimg + (size_t)(j - 1) * h->vn_ncs * 32;
       vn.gate = gate;
       vn.trace = (trace && j == I / 2) ? trace : nullptr;
       HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_fast(vn, h->VM, h->kvn.grid, h->kvn.block, h->kvn.lds, s); }));
       cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
+      cn.cimg = h->cn_cimg + (size_t)j * h->cn_ncs * 32;
       cn.gate = gate;
       cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
       cn.trace = (trace && j == I / 2) ? trace + 3 * nwv : nullptr;

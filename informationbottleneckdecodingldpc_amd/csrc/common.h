@@ -29,6 +29,18 @@ constexpr int kTbl = 8192;        // LDS bytes per IB lookup table (replicated o
 constexpr int kRegion = 4 * kTbl;
 __host__ __device__ constexpr uint32_t slot_off(int s) { return (uint32_t)(s >> 2) * kRegion + (uint32_t)(s & 3); }
 constexpr int regions_of(int nt) { return (nt + 3) >> 2; }
+// Column images (tools/gen_sched.py "Column fetches"): the last cn_ncols(D) / vn_ncols(D) inputs of a
+// node read their shared table's whole column (16 nibbles, ds_read_b64) instead of one entry per
+// chain. 4 KiB of LDS per table image (16 columns x 32 lane copies x 8 B).
+constexpr int kColImg = 4096;
+#ifndef IBL_NC_CN
+#define IBL_NC_CN 0
+#endif
+#ifndef IBL_NC_VN
+#define IBL_NC_VN 0
+#endif
+__host__ __device__ constexpr int cn_ncols(int D) { return (D >= 5 && D <= 8) ? IBL_NC_CN : 0; }
+__host__ __device__ constexpr int vn_ncols(int D) { return (D >= 6 && D <= 8) ? IBL_NC_VN : 0; }
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
 constexpr int kMaxD = 16;
 constexpr int kLightD = 4;        // nodes up to this degree run with a 4-row item buffer         // largest node degree with an unrolled fast-path body
@@ -65,6 +77,9 @@ struct IbFastArgs {
   int32_t* unsat;           // kShards flag words to set when a check is unsatisfied (nullptr: no syndrome)
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
   int32_t nt;               // 32-KiB table regions staged in LDS (4 tables each)
+  const uint32_t* cimg;     // this pass's column images: ncs x 16 columns x 2 dwords (stage_cols)
+  int32_t ncs;              // column images staged after the table regions
+  int8_t ccol[kMaxD + 1][4];// per degree: column image of its i-th column-fetched input
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
   uint64_t* trace;          // diagnostics (IBL_TRACE_WAVES): per wave {start clock, end clock, items}, else nullptr

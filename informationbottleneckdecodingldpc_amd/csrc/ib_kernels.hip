@@ -47,6 +47,23 @@ __device__ __forceinline__ uint32_t luc(uint32_t t, uint32_t q, uint32_t c) {
   asm("v_lshl_or_b32 %0, %1, 11, %2" : "=v"(x) : "v"(t), "v"(q));
   return *(lds8_t*)(size_t)(x + c);
 }
+// Column fetch (tools/gen_sched.py, "Column fetches"): column T(., m) of one table as 16 nibbles
+// (entry t at bits 4t..4t+3), one ds_read_b64 from the bank-replicated column image at byte
+// m*256 + 8*(lane&31) of the table's 4-KiB image; cb = 8*(lane&31) + image base. The 32 lanes of a
+// bank group read 2 of the 64 banks each: conflict free.
+typedef __attribute__((address_space(3))) const uint64_t lds64_t;
+__device__ __forceinline__ uint64_t colf(uint32_t m, uint32_t cb) {
+  uint32_t x;
+  asm("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(x) : "v"(m), "v"(cb));
+  return *(lds64_t*)(size_t)x;
+}
+// entry t of a fetched column, sh = 4t in its low 6 bits (v_lshrrev_b64 reads only those): a
+// previous column result r, whose bits above its nibble hold the next entries, passes as r << 2.
+__device__ __forceinline__ uint32_t csel(uint64_t col, uint32_t sh) {
+  uint64_t r;
+  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "v"(sh), "v"(col));
+  return (uint32_t)r;
+}
 __device__ __forceinline__ uint32_t lds_base(const uint8_t* p) { return (uint32_t)(size_t)(lds8_t*)p; }
 __device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
   if (lds_base(lds) != 0u) __builtin_trap();  // uniform scalar test; never taken without static LDS
@@ -69,6 +86,14 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
   uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
   const int n = nreg * (kRegion / 4);
   for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
+}
+
+// column images: ncs tables x 16 columns x 2 dwords (entries t < 8, t >= 8) replicated for the 32
+// lanes of a bank group: LDS dword c*1024 + m*64 + 2*L + h (see colf)
+__device__ __forceinline__ void stage_cols(uint8_t* dst, const uint32_t* cimg, int ncs) {
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(dst);
+  const int n = ncs * 1024;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = cimg[((i >> 10) << 5) | (((i >> 6) & 15) << 1) | (i & 1)];
 }
 
 // Fast-path message format: T <= 16, so every message is a 4-bit nibble; an edge row stores
@@ -195,16 +220,23 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 
 template <int D>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
-                                        uint32_t (&outw)[D]) {
+                                        const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
 #pragma unroll 1
-  for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, outw, k0);
+  for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
+}
+
+// column-image addresses of the column-fetched inputs of a degree-D node (cb of colf)
+__device__ __forceinline__ void col_bases(const int8_t (&cc)[4], uint32_t lane8c, uint32_t (&cb)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) cb[i] = lane8c + ((uint32_t)cc[i] << 12);
 }
 
 template <int D, class Buf>
-__device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, const Buf& b, int fslot, bool do_par,
-                                           bool& unsat) {
+__device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, const Buf& b,
+                                           int fslot, bool do_par, bool& unsat) {
   constexpr int W = Buf::W;
-  uint32_t outw[D][W], trow[D];
+  uint32_t outw[D][W], trow[D], cb[4];
+  col_bases(a.ccol[D], lane8c, cb);
 #pragma unroll
   for (int w = 0; w < D; ++w) {
     trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
@@ -253,7 +285,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
         o[1] = in[0];
       }
     } else {
-      cn_word<D>(lane4, in, fbase, o);
+      cn_word<D>(lane4, in, fbase, cb, o);
     }
 #pragma unroll
     for (int w = 0; w < D; ++w) outw[w][i] = o[w];
@@ -269,15 +301,17 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 // (:131-136). Schedules as for the check node (vn_group in ib_sched.inc).
 template <int D>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
-                                        uint32_t fbase, uint32_t (&outw)[D]) {
+                                        uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
 #pragma unroll 1
-  for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, outw, k0);
+  for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
 
 template <int D, class Buf>
-__device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, const Buf& b, int fslot) {
+__device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, const Buf& b,
+                                           int fslot) {
   constexpr int W = Buf::W;
-  uint32_t outw[D][W], trow[D];
+  uint32_t outw[D][W], trow[D], cb[4];
+  col_bases(a.ccol[D], lane8c, cb);
 #pragma unroll
   for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   const uint32_t fbase = slot_off(fslot);
@@ -292,7 +326,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, 
         in[j] = b.row[j][i];
         o[j] = 0;
       }
-      vn_word<D>(lane4, in, b.chw[i], fbase, o);
+      vn_word<D>(lane4, in, b.chw[i], fbase, cb, o);
 #pragma unroll
       for (int w = 0; w < D; ++w) outw[w][i] = o[w];
     }
@@ -353,6 +387,19 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // ---------------------------------------------------------------------- kernels
 #define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+#ifndef IBL_MIX
+#define IBL_MIX 0
+#endif
+
+// LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
+__device__ __forceinline__ int* lds_counters(const uint8_t* lds, const IbFastArgs& a) {
+  return reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + (size_t)a.nt * kRegion + (size_t)a.ncs * kColImg);
+}
+__device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
+  if (threadIdx.x < 2) lds_counters(lds, a)[threadIdx.x] = 0;
+  stage_tables(lds, a.img, a.nt);
+  stage_cols(lds + (size_t)a.nt * kRegion, a.cimg, a.ncs);
+}
 
 // Persistent wave loop shared by the CN and VN passes: items (position, chunk) are dealt
 // round-robin to the grid's waves; each iteration prefetches the next item, then computes the
@@ -360,22 +407,22 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // heaviest-first: [0, n_heavy) run with a MAXD-row item buffer, the rest with a kLightD-row one
 // (a degree-2 node then issues 4 row loads, not MAXD).
 template <class Buf, bool VN, bool GATHER, int DLO>
-__device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, int lane, int first, int end, int nw,
-                                         int wpb, int* ctr, bool do_par, bool& unsat, int& items_done) {
+__device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
+                                         int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat, int& items_done) {
   // always inlined: an out-of-line body would take the item by reference through scratch
   auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
     settle(cur);
     if constexpr (VN) {
       switch (cur.d) {
-        case 1: if constexpr (DLO < 1) vn_compute<1>(a, lane4, cur, 0); break;
-#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) vn_compute<D>(a, lane4, cur, a.fslot[D]); break;
+        case 1: if constexpr (DLO < 1) vn_compute<1>(a, lane4, lane8c, cur, 0); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) vn_compute<D>(a, lane4, lane8c, cur, a.fslot[D]); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
       }
     } else {
       switch (cur.d) {
-#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D>(a, lane4, cur, a.fslot[D], do_par, unsat); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D>(a, lane4, lane8c, cur, a.fslot[D], do_par, unsat); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
@@ -430,10 +477,24 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   bool unsat = false;
   constexpr int W = rowW<MAXD>();
   const uint64_t t0 = a.trace ? __builtin_readcyclecounter() : 0;
-  int* ctr = reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + (size_t)a.nt * kRegion);  // 2 phase counters
+  int* ctr = lds_counters(lds, a);  // 2 phase counters
+  // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
+  const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)a.nt * kRegion;
   int mine = 0;
-  ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat, mine);
-  ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par, unsat, mine);
+  // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
+  // degree-2/3 variables, few lookups per byte moved) by HBM. Waves whose index / 4 in the block is
+  // below IBL_MIX take the light share first, so both kinds run side by side on every CU; a wave that
+  // exhausts its first share joins the other (two ticket counters).
+  const bool light_first = VN && ((threadIdx.x >> 8) < IBL_MIX);
+#pragma unroll 1
+  for (int r = 0; r < 2; ++r) {
+    if ((r == 0) != light_first)
+      ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
+                                                      mine);
+    else
+      ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
+                                                   unsat, mine);
+  }
   if (a.trace && lane == 0) {
     const uint64_t t1 = __builtin_readcyclecounter();
     a.trace[3 * gw] = t0;
@@ -457,8 +518,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
-  if (threadIdx.x < 2) reinterpret_cast<int*>(lds + (size_t)a.nt * kRegion)[threadIdx.x] = 0;
-  stage_tables(lds, a.img, a.nt);
+  stage_pass(lds, a);
   __syncthreads();
   ib_pass<MAXD, false, GATHER>(a, lds);
 }
@@ -468,8 +528,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
   lds_at_zero(lds);
-  if (threadIdx.x < 2) reinterpret_cast<int*>(lds + (size_t)a.nt * kRegion)[threadIdx.x] = 0;
-  stage_tables(lds, a.img, a.nt);
+  stage_pass(lds, a);
   __syncthreads();
   ib_pass<MAXD, true, false>(a, lds);
 }

@@ -91,6 +91,51 @@ def test_ib_other_alphabets(eng, reg_H, Tc, T):
     np.testing.assert_array_equal(out, ref)
 
 
+def _mixed_code(cdegs, vdegs, n, seed):
+    """Random irregular code whose check / variable degrees cover the given sets (every fast-path
+    body, incl. the column-fetched inputs of degrees 5..8, and the MAXD=16 bodies). Socket matching;
+    double edges are merged, a draw that leaves a check of degree < 2 is redrawn."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    for _ in range(100):
+        vd = np.concatenate([vdegs, rng.choice(vdegs, n - len(vdegs))])
+        E = int(vd.sum())
+        m = max(int(round(E / np.mean(cdegs))), len(cdegs))   # check total reachable within the degree range
+        cd = np.concatenate([cdegs, rng.choice(cdegs, m - len(cdegs))])
+        while cd.sum() != E:   # move the check total onto E within [min, max] of cdegs
+            i = int(rng.integers(len(cdegs), m))
+            step = 1 if cd.sum() < E else -1
+            if min(cdegs) <= cd[i] + step <= max(cdegs):
+                cd[i] += step
+        rows = rng.permutation(np.repeat(np.arange(m), cd))
+        cols = np.repeat(np.arange(n), vd)
+        H = sp.csr_matrix((np.ones(E, dtype=np.int64), (rows, cols)), shape=(m, n))
+        H.data[:] = 1
+        c = np.diff(H.indptr)
+        v = np.bincount(H.indices, minlength=n)
+        if c.min() >= 2 and v.min() >= 1 and c.max() <= 16 and v.max() <= 16:
+            return H
+    raise RuntimeError("no simple mixed code drawn")
+
+
+@pytest.mark.parametrize("match,cdegs,vdegs,fast", [
+    (False, list(range(2, 17)), list(range(1, 17)), True),       # every body, MAXD=16 path on both sides
+    (True, [3, 5, 6, 7, 8], [1, 2, 3, 5, 6, 7, 8], True),         # MAXD=8, every column-fetch degree, matching
+    (True, [2, 4, 6, 10], [2, 4, 6, 7, 12], True),                # matching, 9 check degrees 2..10 (16 tables)
+])
+@pytest.mark.parametrize("early", [False, True])
+def test_ib_mixed_degrees_fast_path(eng, match, cdegs, vdegs, fast, early):
+    g = graph.build_graph(_mixed_code(np.array(cdegs), np.array(vdegs), 600, seed=len(cdegs)))
+    imax, B = 7, 1100
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=len(vdegs))
+    ch = np.random.default_rng(9).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
+    out, it, dec = _run(eng, g, tb, ch, match, early)
+    assert dec.fast_path == fast
+    assert it == ref_it
+    np.testing.assert_array_equal(out, ref)
+
+
 def test_ib_early_stop_converging(eng, wlan_H):
     """LLR-quantised tables at good SNR: the batch converges before imax; same stop iteration and
     outputs as the oracle, with matching on."""

@@ -14,8 +14,24 @@ after another. This script list-schedules the chains onto L concurrent lanes (cr
 and emits straight-line code with one SSA name per value (no register copies): each time step
 issues the lookups of every running lane for all S sub-slots back to back.
 
-usage: python tools/gen_sched.py [S_cn L_cn [S_vn L_vn]] > informationbottleneckdecodingldpc_amd/csrc/ib_sched.inc
-(measured on DVB-S2: CN S=4 L=2, VN S=2 L=4 — the default)
+Column fetches. Input in_j meets the SAME table in every chain that did not fold it into its
+prefix: B_{j-2}(., in_j) in the out0 chain and in chains w = 1..j-1 of a check node (j uses),
+V_{j-1}(., in_j) likewise for a variable node. For the last NC inputs of a node (cn_ncols(D) /
+vn_ncols(D) in common.h) the kernel reads that table's whole column T(., m = in_j) once - 16
+nibbles, one conflict-free ds_read_b64 of a bank-replicated column image - and selects entry t
+with a 64-bit shift by 4t (csel). Those j lookups then cost one LDS read instead of j (DVB-S2
+degree-7 check: 25 LDS reads -> 16; degree-8 variable: 35 -> 20), paid with one extra VALU per
+lookup; the LDS array, not VALU issue, is what bounds the byte-lookup kernels. Column steps come
+last in every chain (the NC inputs are the last ones folded), so a byte lookup never follows one.
+
+Measured (tools/variants.py nc23/nc22/nc33/s2, DVB-S2 B=8192 i_max=50): column fetches LOSE - CN
+0.464 -> 0.622 ms, VN 0.478 -> 0.526 ms at NC = 2/3 (170.9k -> 140.9k cw/s). The 64-bit shift and the
+nibble masks cost more VALU issue than the saved LDS reads return, so the default is NC = 0 (no
+column images, the byte-lookup schedules of before); the option stays for other code profiles.
+
+usage: python tools/gen_sched.py [S_cn L_cn S_vn L_vn [NC_cn NC_vn]] > informationbottleneckdecodingldpc_amd/csrc/ib_sched.inc
+(measured on DVB-S2: CN S=4 L=2, VN S=2 L=4, NC 0 0; NC_cn / NC_vn must equal IBL_NC_CN / IBL_NC_VN
+of the build that includes the file - the file static_asserts it)
 """
 import sys
 
@@ -26,28 +42,35 @@ def slot_off(l):
     return (l >> 2) * 32768 + (l & 3)
 
 
+def cn_ncols(D, nc):
+    return nc if 5 <= D <= 8 else 0
+
+
+def vn_ncols(D, nc):
+    return nc if 6 <= D <= 8 else 0
+
+
 def cn_chains(D):
-    def slot(j, l):
-        return "0u" if j == D - 1 else ("fbase" if l == D - 3 else f"{slot_off(l)}u")
-    ch = [dict(id="o0", start=("nib", 1), steps=[("q", j, slot(j, j - 2)) for j in range(2, D)], out=0),
-          dict(id="P", start=("nib", 0), steps=[("q", w, slot(w, w - 1)) for w in range(1, D - 1)], out=D - 1,
-               exports={i: f"P{i + 2}" for i in range(D - 2)})]     # after step i: P_{i+2}
+    def st(j, l):
+        sl = "0u" if j == D - 1 else ("fbase" if l == D - 3 else f"{slot_off(l)}u")
+        return ("q", j, sl, l)
+    ch = [dict(id="o0", start=("nib", 1), steps=[st(j, j - 2) for j in range(2, D)], out=0),
+          dict(id="P", start=("nib", 0), steps=[st(w, w - 1) for w in range(1, D - 1)], out=D - 1)]
     for w in range(1, D - 1):
-        st = ("nib", 0) if w == 1 else ("val", "P", w - 2)          # P_w = P chain after step w-2
-        ch.append(dict(id=f"c{w}", start=st, steps=[("q", j, slot(j, j - 2)) for j in range(w + 1, D)], out=w))
+        s0 = ("nib", 0) if w == 1 else ("val", "P", w - 2)              # P_w = P chain after step w-2
+        ch.append(dict(id=f"c{w}", start=s0, steps=[st(j, j - 2) for j in range(w + 1, D)], out=w))
     return ch
 
 
 def vn_chains(D):
-    def slot(j, l):
-        return "0u" if j == D - 1 else ("fbase" if l == D - 2 else f"{slot_off(l)}u")
-    ch = [dict(id="o0", start=("chan",), steps=[("c", 1, slot(1, 0))] + [("q", j, slot(j, j - 1)) for j in range(2, D)],
-               out=0),
-          dict(id="Q", start=("chan",), steps=[("c", 0, slot(0, 0))] + [("q", w, slot(w, w)) for w in range(1, D - 1)],
-               out=D - 1)]
+    def st(op, j, l):
+        sl = "0u" if j == D - 1 else ("fbase" if l == D - 2 else f"{slot_off(l)}u")
+        return (op, j, sl, l)
+    ch = [dict(id="o0", start=("chan",), steps=[st("c", 1, 0)] + [st("q", j, j - 1) for j in range(2, D)], out=0),
+          dict(id="Q", start=("chan",), steps=[st("c", 0, 0)] + [st("q", w, w) for w in range(1, D - 1)], out=D - 1)]
     for w in range(1, D - 1):
-        ch.append(dict(id=f"c{w}", start=("val", "Q", w - 1),       # Q_w = Q chain after step w-1
-                       steps=[("q", j, slot(j, j - 1)) for j in range(w + 1, D)], out=w))
+        ch.append(dict(id=f"c{w}", start=("val", "Q", w - 1),           # Q_w = Q chain after step w-1
+                       steps=[st("q", j, j - 1) for j in range(w + 1, D)], out=w))
     return ch
 
 
@@ -60,13 +83,11 @@ def schedule(chains, L):
     ready_at = {}
     for c in chains:
         ready_at[c["id"]] = 0 if c["start"][0] in ("nib", "chan") else None
-    done_step = {}   # (chain, step) -> time
     running = []     # [chain_id, next_step]
     pending = [c["id"] for c in chains]
     out = []
     t = 0
     while pending or running:
-        # fill lanes
         cand = [cid for cid in pending if ready_at[cid] is not None and ready_at[cid] <= t]
         cand.sort(key=lambda cid: (-by_id[cid]["prio"], chains.index(by_id[cid])))
         while len(running) < L and cand:
@@ -78,7 +99,6 @@ def schedule(chains, L):
         issued = []
         for r in running:
             issued.append((r[0], r[1]))
-            done_step[(r[0], r[1])] = t
             r[1] += 1
         out.append((t, issued))
         # exports become available next step
@@ -92,16 +112,29 @@ def schedule(chains, L):
     return out
 
 
-def emit_body(kind, D, S, L):
+def emit_body(kind, D, S, L, NC):
     chains = cn_chains(D) if kind == "cn" else vn_chains(D)
     by_id = {c["id"]: c for c in chains}
     sched = schedule(chains, L)
+    back = 2 if kind == "cn" else 1          # input j meets table j-back in every non-prefix chain
+
+    def is_col(step):
+        op, j, _, l = step
+        return op == "q" and j >= D - NC and l == j - back
+
+    for c in chains:   # column steps are the tail of every chain
+        cols = [is_col(s) for s in c["steps"]]
+        assert cols == sorted(cols), (kind, D, c["id"])
     lines = []
-    qidx = sorted({st[1] for c in chains for st in c["steps"]})
-    for j in qidx:
+    u8_in = sorted({s[1] for c in chains for s in c["steps"] if not is_col(s)})
+    col_in = sorted({s[1] for c in chains for s in c["steps"] if is_col(s)})
+    for j in u8_in:
         for s in range(S):
             extra = " + fbase" if j == D - 1 else ""
             lines.append(f"  const uint32_t q{j}_{s} = qidx(nib(in[{j}], k0 + {s}), lane4){extra};")
+    for j in col_in:
+        for s in range(S):
+            lines.append(f"  const uint64_t C{j}_{s} = colf(nib(in[{j}], k0 + {s}), cb[{j - (D - NC)}]);")
     if kind == "vn":
         for s in range(S):
             lines.append(f"  const uint32_t c_{s} = nib(chw, k0 + {s}) << 11;")
@@ -121,18 +154,20 @@ def emit_body(kind, D, S, L):
         lines.append(f"  // step {t}: " + ", ".join(f"{cid}[{k}]" for cid, k in issued))
         for cid, k in issued:
             c = by_id[cid]
-            op, j, sl = c["steps"][k]
+            step = c["steps"][k]
+            op, j, sl, _ = step
             for s in range(S):
                 if op == "c":
                     expr = f"lu(c_{s} + q{j}_{s}, {sl})"
                 else:
                     prev = start_val(c, s) if k == 0 else name(cid, k - 1, s)
-                    expr = f"luc({prev}, q{j}_{s}, {sl})"
+                    expr = f"csel(C{j}_{s}, {prev} << 2)" if is_col(step) else f"luc({prev}, q{j}_{s}, {sl})"
                 lines.append(f"  const uint32_t {name(cid, k, s)} = {expr};")
         for cid, k in issued:
             c = by_id[cid]
             if k == len(c["steps"]) - 1:
-                vals = [name(cid, k, s) for s in range(S)]
+                col = is_col(c["steps"][k])
+                vals = [f"({name(cid, k, s)} & 15u)" if col else name(cid, k, s) for s in range(S)]
                 pk = vals[0]
                 for s in range(1, S):
                     pk = f"{pk} | ({vals[s]} << {4 * s})"
@@ -141,34 +176,41 @@ def emit_body(kind, D, S, L):
 
 
 def main():
-    """args: S_cn L_cn [S_vn L_vn] (group size and chain lanes per kernel, for degrees <= 8; larger
-    degrees use S = 2, L = 4 so the MAXD = 16 bodies keep their occupancy)."""
+    """args: S_cn L_cn [S_vn L_vn [NC_cn NC_vn]] (group size and chain lanes per kernel, for degrees
+    <= 8; larger degrees use S = 2, L = 4 so the MAXD = 16 bodies keep their occupancy; column-fetched
+    trailing inputs per check / variable node)."""
     a = [int(x) for x in sys.argv[1:]] or [4, 2, 2, 4]
     Sc, Lc = a[0], a[1]
     Sv, Lv = (a[2], a[3]) if len(a) >= 4 else (Sc, Lc)
+    NCc, NCv = (a[4], a[5]) if len(a) >= 6 else (0, 0)
 
     def cfg(S, L, D):
         return (S, L) if D <= 8 else (2, 4)
     print(f"// GENERATED by tools/gen_sched.py {' '.join(sys.argv[1:])} -- do not edit.")
     print(f"// Fold schedules of the IB fast path (degrees <= 8): CN groups of {Sc} codewords with up to {Lc}")
     print(f"// chains in flight, VN groups of {Sv} codewords with up to {Lv}; degrees > 8: 2 codewords, 4 chains.")
+    print(f"// Column fetches: the last {NCc} inputs of checks of degree 5..8, the last {NCv} of variables of degree 6..8.")
+    print(f"static_assert(cn_ncols(7) == {cn_ncols(7, NCc)} && vn_ncols(8) == {vn_ncols(8, NCv)},")
+    print("              \"ib_sched.inc was generated for other IBL_NC_CN / IBL_NC_VN\");")
     print(f"__host__ __device__ constexpr int cn_sched_s(int D) {{ return D <= 8 ? {Sc} : 2; }}")
     print(f"__host__ __device__ constexpr int vn_sched_s(int D) {{ return D <= 8 ? {Sv} : 2; }}")
     print("template <int D> __device__ __forceinline__ void cn_group(uint32_t lane4, const uint32_t (&in)[D],")
-    print("                                                         uint32_t fbase, uint32_t (&o)[D], int k0);")
+    print("                                                         uint32_t fbase, const uint32_t (&cb)[4],")
+    print("                                                         uint32_t (&o)[D], int k0);")
     print("template <int D> __device__ __forceinline__ void vn_group(uint32_t lane4, const uint32_t (&in)[D],")
-    print("                                                         uint32_t chw, uint32_t fbase, uint32_t (&o)[D],")
-    print("                                                         int k0);")
+    print("                                                         uint32_t chw, uint32_t fbase, const uint32_t (&cb)[4],")
+    print("                                                         uint32_t (&o)[D], int k0);")
     for D in range(3, KMAXD + 1):
         print(f"template <> __device__ __forceinline__ void cn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
-        print(f"                                                         uint32_t fbase, uint32_t (&o)[{D}], int k0) {{")
-        print("\n".join(emit_body("cn", D, *cfg(Sc, Lc, D))))
+        print("                                                         uint32_t fbase, const uint32_t (&cb)[4],")
+        print(f"                                                         uint32_t (&o)[{D}], int k0) {{")
+        print("\n".join(emit_body("cn", D, *cfg(Sc, Lc, D), cn_ncols(D, NCc))))
         print("}")
     for D in range(2, KMAXD + 1):
         print(f"template <> __device__ __forceinline__ void vn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
-        print(f"                                                         uint32_t chw, uint32_t fbase,")
+        print("                                                         uint32_t chw, uint32_t fbase, const uint32_t (&cb)[4],")
         print(f"                                                         uint32_t (&o)[{D}], int k0) {{")
-        print("\n".join(emit_body("vn", D, *cfg(Sv, Lv, D))))
+        print("\n".join(emit_body("vn", D, *cfg(Sv, Lv, D), vn_ncols(D, NCv))))
         print("}")
 
 

@@ -14,6 +14,9 @@ for s in $STEPS; do
     tests)
       timeout -k 10 900 python -m pytest $R/tests -m gpu -q --timeout 400 -p no:cacheprovider > $O/pytest.log 2>&1
       rc=$?; echo "pytest rc=$rc $(tail -1 $O/pytest.log)" >> $O/summary.txt; crash $rc pytest;;
+    ibtests)
+      timeout -k 10 600 python -u -m pytest $R/tests/test_gpu_ib.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_ib.log 2>&1
+      rc=$?; echo "pytest ib rc=$rc $(tail -1 $O/pytest_ib.log)" >> $O/summary.txt; crash $rc pytest_ib; [ $rc = 0 ] || exit $rc;;
     enctests)
       timeout -k 10 600 python -m pytest $R/tests/test_gpu_encoder.py -m gpu -x -q --timeout 300 -p no:cacheprovider > $O/pytest_enc.log 2>&1
       rc=$?; echo "pytest enc rc=$rc $(tail -1 $O/pytest_enc.log)" >> $O/summary.txt; crash $rc pytest_enc; [ $rc = 0 ] || exit $rc;;

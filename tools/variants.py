@@ -1,6 +1,7 @@
 """Build kernel variants of libibldpc.so side by side (in-tree, so they travel to the GPU box) for A/B
 timing: `python tools/variants.py` then `IBLDPC_LIB=<path> python bench.py ...`."""
 import os
+import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -15,13 +16,27 @@ VARIANTS = {
     "w2b": ["IBL_W=2", "IBL_LB8=512"],
     "wpe5": ["IBL_WPE8=5"],
     "wpe6": ["IBL_WPE8=6"],
+    # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
+    # Measured on DVB-S2 (B=8192, i_max=50): nc00 170.9k cw/s (CN 0.464 / VN 0.478 ms), nc23 140.9k
+    # (0.622 / 0.526), nc22 142.0k, nc33 132.3k, s2 156.5k -> the default build keeps NC = 0.
+    "nc23": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc23.inc"'],
+    "nc22": ["IBL_NC_CN=2", "IBL_NC_VN=2", 'IBL_SCHED_FILE="ib_sched_nc22.inc"'],
+    "nc33": ["IBL_NC_CN=3", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc33.inc"'],
+    "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
 }
+# gen_sched.py arguments of the variants that need their own schedule file
+SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3"}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     outdir = os.path.join(_build.PKG, "variants")
     os.makedirs(outdir, exist_ok=True)
     for n in names:
+        if n in SCHED_ARGS:
+            inc = os.path.join(_build.CSRC, f"ib_sched_{n}.inc")
+            with open(inc, "w") as f:
+                subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gen_sched.py"),
+                                *SCHED_ARGS[n].split()], stdout=f, check=True)
         lib = os.path.join(outdir, f"libibldpc_{n}.so")
         _build.build(defines=VARIANTS[n], lib=lib, tag=n, force="--force" in os.environ.get("VARIANT_FLAGS", ""))
         print(lib)
