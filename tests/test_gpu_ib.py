@@ -121,7 +121,9 @@ def _mixed_code(cdegs, vdegs, n, seed):
 @pytest.mark.parametrize("match,cdegs,vdegs,fast", [
     (False, list(range(2, 17)), list(range(1, 17)), True),       # every body, MAXD=16 path on both sides
     (True, [3, 5, 6, 7, 8], [1, 2, 3, 5, 6, 7, 8], True),         # MAXD=8, every column-fetch degree, matching
-    (True, [2, 4, 6, 10], [2, 4, 6, 7, 12], True),                # matching, 9 check degrees 2..10 (16 tables)
+    # matching, 9 variable degrees up to 12: 10 fold + 9 composed tables = 5 LDS regions (160 KiB) plus
+    # the work counters exceed the CU's LDS, so the decoder takes the generic path (still bit-exact)
+    (True, [2, 4, 6, 10], [2, 4, 6, 7, 12], False),
 ])
 @pytest.mark.parametrize("early", [False, True])
 def test_ib_mixed_degrees_fast_path(eng, match, cdegs, vdegs, fast, early):
