@@ -57,6 +57,9 @@ for s in $STEPS; do
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 3 > $O/bench_prof.json 2> $O/prof.err)
       rc=$?; echo "rocprof rc=$rc" >> $O/summary.txt; crash $rc rocprof;;
+    profc3)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_c3 -o run --output-format csv -- python3 $R/bench.py --config C3 --no-cpu-baseline --steps 2 > $O/bench_prof_c3.json 2> $O/prof_c3.err)
+      rc=$?; echo "rocprof C3 rc=$rc" >> $O/summary.txt; crash $rc rocprof_c3;;
     proffloat)
       for k in minsum bp; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_$k -o run --output-format csv -- python3 $R/bench.py --kind $k --no-cpu-baseline --steps 2 > $O/bench_prof_$k.json 2> $O/prof_$k.err)
