@@ -143,6 +143,35 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put
       }
       put(w, o);
     }
+  } else if constexpr (sizeof(F) == 4) {
+    // fp32 BP: forward-backward box-plus, 3(D-2) operations instead of the (D-2)(D+3)/2 of the
+    // reference's per-output folds (degree 7: 15 vs 25; each costs 4 transcendentals). Box-plus is
+    // commutative and associative, and |a [+] b| <= min(|a|,|b|) keeps every partial result inside
+    // the clamp for clamped inputs, so only the fp32 rounding differs from the reference order
+    // (within the tolerance of tests/test_gpu_float.py; the fp64 build keeps the exact order below).
+    F S[D][N], P[N];   // S[j] = m_j [+] ... [+] m_{D-1}, j >= 1
+#pragma unroll
+    for (int s = 0; s < N; ++s) S[D - 1][s] = m[D - 1][s];
+#pragma unroll
+    for (int j = D - 2; j >= 1; --j)
+#pragma unroll
+      for (int s = 0; s < N; ++s) S[j][s] = boxplus(m[j][s], S[j + 1][s], lm);
+#pragma unroll
+    for (int s = 0; s < N; ++s) o[s] = clampllr(S[1][s], lm);
+    put(0, o);
+#pragma unroll
+    for (int s = 0; s < N; ++s) P[s] = m[0][s];
+#pragma unroll
+    for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+      for (int s = 0; s < N; ++s) o[s] = clampllr(boxplus(P[s], S[w + 1][s], lm), lm);
+      put(w, o);
+#pragma unroll
+      for (int s = 0; s < N; ++s) P[s] = boxplus(m[w][s], P[s], lm);
+    }
+#pragma unroll
+    for (int s = 0; s < N; ++s) o[s] = clampllr(P[s], lm);
+    put(D - 1, o);
   } else {
     // BP sequential box-plus folds with prefix sharing (kernels_min_and_BP.cl:63-69)
     F t[N], P[N];
