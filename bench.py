@@ -2,12 +2,15 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B] [--imax I]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
-    python bench.py --config C2|C3|C5                      (BASELINE.json's other GPU configs)
+    python bench.py --config C1|C2|C3|C5                   (BASELINE.json's other configs)
 
-Default = BASELINE config C4 (the headline metric). The other presets measure the remaining GPU
-configs of BASELINE.json: C2 regular (3,6) N=8000 IB T=16 i_max=50, 65536 codewords; C3 WLAN
-N=1944 (802.11n-structured, Z=81) min-sum fp32 i_max=50, 262144 codewords; C5 DVB-S2 BP fp32
-i_max=100, 8192 codewords per GPU.
+Default = BASELINE config C4 (the headline metric). The other presets measure the remaining
+configs of BASELINE.json: C1 regular (3,6) N=8000 IB T=16 i_max=10, 1000 codewords (the reference's
+CPU case: its numpy decode_on_host, restated in oracle/host_numpy.py, is the cpu_baseline, one
+process per host core, next to the GPU decoding the same 1000 codewords); C2 regular (3,6) N=8000
+IB T=16 i_max=50, 65536 codewords; C3 WLAN N=1944 (802.11n-structured, Z=81) min-sum fp32
+i_max=50, 262144 codewords; C5 DVB-S2 BP fp32 i_max=100, 8192 codewords per GPU. The regular
+configs run without matching (the reference's regular class has none).
 
 A "step" = one decode call of B codewords per GPU (DVB-S2-structured N=64800 R=1/2 code,
 T=16 lookup tables with matching, i_max=50 fixed iterations — early stop off, as the roofline
@@ -17,8 +20,11 @@ as N grows (weak scaling); codeword ranges are disjoint per rank and no collecti
 the timed region.
 
 Rank 0 prints one JSON line with the whole-job codewords/s, the algorithmic HBM GB/s, the
-roofline of the dominant kernel (HIP-event timed per launch inside the timed region) and the
-CPU baseline (the C oracle — a port of the reference kernels — on a bounded sample).
+roofline of the dominant kernel (HIP-event timed per launch inside the timed region; priced at the
+bytes the kernel actually moves: 4-bit messages on the IB fast path, LDS bytes for the fused on-chip
+float kernel) and the CPU baseline on a bounded sample: the reference's numpy host path
+(restated) where the reference has one (regular IB: C1, C2), else the C oracle (a port of the
+reference's OpenCL kernels).
 """
 from __future__ import annotations
 
@@ -46,19 +52,22 @@ def parse():
     p.add_argument("--ebn0", type=float, default=0.6)
     p.add_argument("--kind", choices=["ib", "minsum", "bp"], default="ib")
     p.add_argument("--code", choices=["dvbs2", "regular", "wlan"], default="dvbs2")
-    p.add_argument("--config", choices=["C2", "C3", "C4", "C5"], default=None,
+    p.add_argument("--config", choices=["C1", "C2", "C3", "C4", "C5"], default=None,
                    help="BASELINE.json config preset (sets --code/--kind/--imax/--batch-per-gpu)")
     p.add_argument("--no-match", action="store_true")
     p.add_argument("--float-path", choices=["auto", "passes", "fused"], default="auto",
                    help="float decoders: fused on-chip kernel when the code fits in LDS (auto), or per-pass launches")
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
+    p.add_argument("--cpu-procs", type=int, default=0, help="numpy host baseline processes (0 = min(16, host CPUs))")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     a = p.parse_args()
-    presets = {"C2": ("regular", "ib", 50, 65536), "C3": ("wlan", "minsum", 50, 262144),
-               "C4": ("dvbs2", "ib", 50, 8192), "C5": ("dvbs2", "bp", 100, 8192)}
+    presets = {"C1": ("regular", "ib", 10, 1000), "C2": ("regular", "ib", 50, 65536),
+               "C3": ("wlan", "minsum", 50, 262144), "C4": ("dvbs2", "ib", 50, 8192), "C5": ("dvbs2", "bp", 100, 8192)}
     if a.config:
         a.code, a.kind, a.imax, a.batch_per_gpu = presets[a.config]
+        if a.config in ("C1", "C2"):
+            a.no_match = True      # Discrete_LDPC_Decoder_class (regular) has no matching step
     return a
 
 
@@ -79,6 +88,207 @@ def make_code(name):
 def bytes_per_cw(n_e: int, n_v: int, imax: int, w: int) -> int:
     """i_max·(4·E·w_m + N·w_c) + N·(w_c + w_o)."""
     return imax * (4 * n_e * w + n_v * w) + n_v * (w + w)
+
+
+LDS_CLK_GHZ = 2.4          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
+NUM_CUS = 256
+
+
+def _pmc_traffic(path, kind, kname, B, fmt):
+    """Per-launch HBM bytes of `kname` from the committed rocprofv3 PMC summary, when it was measured
+    on the same kernel, batch and message format (else None)."""
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            ent = json.load(fh).get(kind, {}).get(kname)
+        if ent and int(ent.get("batch", -1)) == B and ent.get("format") == fmt:
+            return ent.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec):
+    """Roofline of the dominant kernel, priced at the bytes it actually moves.
+
+    Per-pass kernels (HBM-bound by design): check pass reads E message rows and writes E; variable
+    pass reads E rows + N channel rows and writes E (SURVEY §8(d) per-unit figures), x B codewords,
+    at the stored width (u4 fast path, u8 generic, fp32 float). The u8-equivalent of SURVEY §8(d)'s
+    fixed reporting width is kept as a secondary field. The fused on-chip float kernel keeps every
+    message in LDS: its roofline is the LDS's (16-B slot reads at 256 B/clk/CU, 16-B slot writes at
+    79 B/clk/CU, MI355X_MICROARCH.md §LDS), with its HBM bytes (channel in, APP out) reported beside."""
+    cn_bytes_u8 = 2 * g.n_e * w * B
+    vn_bytes_u8 = (2 * g.n_e * w + n_v * w) * B
+    if fused:
+        # one launch decodes the whole batch: L = imax-1 check passes, L-1 variable passes (16-B slots,
+        # N codewords per slot), plus send (E+N slot writes) and the APP output (E+N slot reads)
+        L = I - 1
+        E = g.n_e
+        slots_r = L * E + max(L - 1, 0) * (E + n_v) + (E + n_v)
+        slots_w = (E + n_v) + L * E + max(L - 1, 0) * E
+        groups = -(-B // 4)
+        rd, wr = 16 * slots_r * groups, 16 * slots_w * groups
+        t = cn_avg * 1e-3
+        peak = (rd + wr) / (rd / 256 + wr / 79) * NUM_CUS * LDS_CLK_GHZ   # GB/s at the instruction mix
+        ach = (rd + wr) / t / 1e9 if t > 0 else 0.0
+        return {"bound": "lds", "kernel": "fl_fused", "achieved": round(ach, 1), "peak": round(peak, 1),
+                "unit": "GB/s", "frac": round(ach / peak, 4), "traffic": None,
+                "bytes_per_launch": rd + wr, "lds_read_bytes": rd, "lds_write_bytes": wr,
+                "avg_launch_ms": round(cn_avg, 4),
+                "hbm": {"bytes_per_launch": 2 * n_v * 4 * B, "achieved": round(2 * n_v * 4 * B / t / 1e9, 1) if t > 0 else 0.0,
+                        "peak": HBM_PEAK_GBPS},
+                "note": "fused on-chip decoder: messages of 4 codewords per workgroup stay in LDS for all "
+                        "iterations; LDS roofline at this kernel's 16-B read/write mix (MI355X_MICROARCH.md §LDS)",
+                "launches": {"fused": cn_n}}
+    if vn_ms >= cn_ms:
+        kname = "ib_vn_fast" if fmt == "u4" else ("ib_vn_gen" if a.kind == "ib" else "fl_vn")
+        kavg, ku8 = vn_avg, vn_bytes_u8
+    else:
+        kname = "ib_cn_fast" if fmt == "u4" else ("ib_cn_gen" if a.kind == "ib" else "fl_cn")
+        kavg, ku8 = cn_avg, cn_bytes_u8
+    kbytes = int(ku8 * ws / w)
+    t = kavg * 1e-3
+    ach = kbytes / t / 1e9 if t > 0 else 0.0
+    roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": _pmc_traffic(a.pmc, a.kind, kname, B, fmt),
+            "bytes_per_launch": kbytes, "format": fmt, "avg_launch_ms": round(kavg, 4),
+            "u8_equivalent": {"bytes_per_launch": ku8, "achieved": round(ku8 / t / 1e9, 1) if t > 0 else 0.0,
+                              "note": "SURVEY §8(d)'s fixed u8 reporting width; not the bytes this kernel moves"}
+            if fmt == "u4" else None,
+            "launches": {"cn": cn_n, "vn": vn_n},
+            "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}}
+    if fmt == "u4":
+        # table lookups per codeword and pass of the fast path (prefix sharing, matching composed), per CU
+        # and clock at the max clock; the LDS serves at most 32 conflict-free ds_read_u8 lanes/clk/CU
+        def cn_lk(d):
+            return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
+
+        def vn_lk(d):
+            return 0 if d == 1 else (d - 1) + d * (d - 1) // 2
+        lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
+        avg = {"cn": cn_avg, "vn": vn_avg}
+        roof["lds_lookups_per_clk_per_cu"] = {k: round(lk[k] / (avg[k] * 1e-3) / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2)
+                                              for k in lk}
+        roof["lds_lookups_per_clk_per_cu"]["ceiling"] = 32.0
+    return roof
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ---- numpy host baseline workers (spawned processes: they never touch the GPU)
+_HOST = {}
+
+
+def _host_init(arrs, Tc, T, imax, cn_lut, vn_lut, regular):
+    import types
+    from oracle.host_numpy import HostDecoder
+    _HOST["dec"] = HostDecoder(types.SimpleNamespace(**arrs), Tc, T, imax, cn_lut, vn_lut, regular=regular)
+
+
+def _host_ready(_):
+    return os.getpid()
+
+
+def _host_decode(cols):
+    dec = _HOST["dec"]
+    return np.stack([dec.decode(c) for c in cols], axis=1)
+
+
+def numpy_host_baseline(g, tb, x_host, imax, regular, procs):
+    """The reference's CPU decode path (decode_on_host, oracle/host_numpy.py): per-core rate measured
+    in this process, aggregate rate with `procs` single-threaded worker processes (spawned, so they
+    hold no GPU state) decoding the sample's codewords one per call."""
+    import multiprocessing as mp
+    from oracle.host_numpy import HostDecoder
+    keys = ("n_v", "n_e", "cn_deg", "cn_start", "tgt_cn", "vn_deg", "vn_start", "tgt_vn")
+    arrs = {k: getattr(g, k) for k in keys}
+    dec = HostDecoder(g, tb.Tc, tb.T, imax, tb.cn, tb.vn, regular=regular)
+    S = x_host.shape[1]
+    k1 = max(1, min(S, 8))
+    dec.decode(x_host[:, 0])
+    t1 = time.perf_counter()
+    for c in range(k1):
+        dec.decode(x_host[:, c])
+    per_core = k1 / (time.perf_counter() - t1)
+    for v in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
+    ctx = mp.get_context("spawn")
+    chunks = [[x_host[:, c] for c in range(i, S, procs)] for i in range(procs)]
+    with ctx.Pool(procs, initializer=_host_init,
+                  initargs=(arrs, tb.Tc, tb.T, imax, tb.cn, tb.vn, regular)) as pool:
+        pool.map(_host_ready, range(procs), chunksize=1)
+        t1 = time.perf_counter()
+        parts = pool.map(_host_decode, chunks, chunksize=1)
+        wall = time.perf_counter() - t1
+    outs = np.zeros((g.n_v, S), dtype=np.int64)
+    for i, p_ in enumerate(parts):
+        if p_.size:
+            outs[:, i::procs] = p_
+    return outs, per_core, S / wall, wall
+
+
+def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
+    """Bounded-sample CPU baseline on this box's host cores (reported beside the GPU, not a target)."""
+    from informationbottleneckdecodingldpc_amd import tables
+    from oracle import oracle
+    host = (lambda S_: src[:, :S_].cpu().numpy().astype(np.int32 if a.kind == "ib" else np.float64))  # noqa: E731
+    ncpu = os.cpu_count() or 1
+    if a.kind == "ib" and a.code == "regular" and not match:
+        # the reference's own CPU path: numpy decode_on_host (regular class), one codeword per call
+        procs = a.cpu_procs or min(16, ncpu)
+        tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+        per_cw_s = 0.0028 * I                         # ~2.8 ms per (3,6) N=8000 iteration per core
+        S = int(min(B, a.cpu_sample, max(procs, 30.0 / per_cw_s)))   # ~30 s of CPU work
+        if a.config == "C1":
+            S = min(B, a.cpu_sample, 1000)            # C1 IS 1000 codewords on the CPU path
+        x = host(S)
+        ref, per_core, agg, wall = numpy_host_baseline(g, tbh, x, I, True, procs)
+        same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int64)))
+        return {"value": round(agg, 3), "unit": "codewords/s", "cores": procs, "kind": "port",
+                "per_core": round(per_core, 3), "cpu_model": _cpu_model(), "host_cpus": ncpu,
+                "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, no matching, fixed iterations; "
+                          f"the reference's numpy decode_on_host (Discrete_LDPC_decoder_class, restated in "
+                          f"oracle/host_numpy.py, bit-identical to the reference's outputs), one codeword per call, "
+                          f"{procs} single-threaded processes, {wall:.1f} s wall; outputs equal GPU: {same}"}
+    nthreads = min(16, ncpu)
+    # bounded sample: a 16-codeword calibration run sizes the measured sample to ~12 s of CPU work
+    if a.kind == "ib":
+        tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+        dec_cpu = lambda x: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nthreads)  # noqa: E731
+    else:
+        dec_cpu = lambda x: oracle.float_decode(g, 0 if a.kind == "minsum" else 1, I, x,  # noqa: E731
+                                                early_stop=False, nthreads=nthreads)
+    S0 = min(16, B)
+    t1 = time.perf_counter()
+    dec_cpu(host(S0))
+    cal = time.perf_counter() - t1
+    S = int(max(S0, min(B, a.cpu_sample, S0 * 12.0 / max(cal, 1e-3))))
+    x_cpu = host(S)
+    t1 = time.perf_counter()
+    ref = dec_cpu(x_cpu)
+    cpu_s = time.perf_counter() - t1
+    if a.kind == "ib":
+        same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int32)))
+        what = (f"oracle/ib_oracle.c (C+OpenMP restatement of the reference OpenCL kernels; the reference's "
+                f"own numpy host path cannot decode this code or has no matching); outputs equal GPU: {same}")
+    else:
+        agree = float(np.mean((ref < 0) == (out[:, :S].cpu().numpy() < 0)))
+        what = (f"oracle/ib_oracle.c fp64 restatement of kernels_min_and_BP.cl (the reference's float host "
+                f"paths are broken, SURVEY App. C3); hard decisions equal to the GPU's fp32: {agree:.6f}")
+    return {"value": round(S / cpu_s, 3), "unit": "codewords/s", "cores": nthreads, "kind": "port",
+            "cpu_model": _cpu_model(), "host_cpus": ncpu,
+            "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, fixed iterations; {what}; "
+                      f"{cpu_s:.1f} s wall"}
 
 
 def main():
@@ -169,82 +379,19 @@ def main():
     value = world * B * a.steps / elapsed
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
-    # SURVEY §8(d) per-unit figures (u8 messages for IB, fp32 for float) x codewords per launch
-    cn_bytes = 2 * g.n_e * w * B
-    vn_bytes = (2 * g.n_e * w + n_v * w) * B
-    # bytes actually stored by this build: the IB fast path keeps 4-bit messages/channel values
-    ws = 0.5 if (a.kind == "ib" and getattr(dec, "fast_path", False)) else w
-    fmt = {0.5: "u4", 1: "u8", 4: "f32"}[ws]
     fused = a.kind != "ib" and dec.fused
-    if fused:
-        # one fl_fused launch decodes the batch with the messages in LDS: its algorithmic bytes are the
-        # whole decode's (SURVEY §8(d) per codeword x B); HBM moves only channel in + APP out
-        kname, kavg, kbytes, kstored = "fl_fused", cn_avg, bpc * B, 2 * n_v * w * B
-        fmt = "f32 (messages in LDS)"
-    elif vn_ms >= cn_ms:
-        kname, kavg, kbytes, kstored = ("ib_vn_fast" if a.kind == "ib" else "fl_vn"), vn_avg, vn_bytes, int(vn_bytes * ws / w)
-    else:
-        kname, kavg, kbytes, kstored = ("ib_cn_fast" if a.kind == "ib" else "fl_cn"), cn_avg, cn_bytes, int(cn_bytes * ws / w)
-    achieved = kbytes / (kavg * 1e-3) / 1e9 if kavg > 0 else 0.0
-    achieved_stored = kstored / (kavg * 1e-3) / 1e9 if kavg > 0 else 0.0
-    traffic = None
-    if os.path.exists(a.pmc):
-        try:
-            with open(a.pmc) as fh:
-                pm = json.load(fh)
-            ent = pm.get(a.kind, {}).get(kname)
-            if ent and int(ent.get("batch", -1)) == B and ent.get("format") == fmt:
-                traffic = ent.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    lds = None
-    if a.kind == "ib" and getattr(dec, "fast_path", False):
-        # table lookups per codeword and pass of the fast path (prefix sharing, matching composed)
-        def cn_lk(d):
-            return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
-        def vn_lk(d):
-            return 0 if d == 1 else (d - 1) + d * (d - 1) // 2
-        lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
-        avg = {"cn": cn_avg, "vn": vn_avg}
-        # per CU and clock at the 2.4 GHz max clock, 256 CUs; LDS ceiling 32 conflict-free ds_read_u8 lanes/clk/CU
-        lds = {k: round(lk[k] / (avg[k] * 1e-3) / (256 * 2.4e9), 2) for k in lk}
-        lds["ceiling"] = 32.0
+    fast = a.kind == "ib" and getattr(dec, "fast_path", False)
+    # bytes per stored message / channel value as this build moves them: the IB fast path keeps 4-bit
+    # nibbles (2 codewords per byte), the generic IB path u8, the float paths fp32
+    ws = 0.5 if fast else w
+    fmt = "u4" if fast else ("u8" if a.kind == "ib" else "f32")
+    if a.kind == "ib":
+        dtype = fmt
+    roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec)
     cpu = None
     code_name, code_desc = CODES[a.code]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle import oracle
-        nthreads = min(16, os.cpu_count() or 1)
-        # bounded sample: a 16-codeword calibration run sizes the measured sample to ~12 s of CPU work
-        # (--cpu-sample caps it)
-        if a.kind == "ib":
-            tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
-            dec_cpu = lambda x: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nthreads)  # noqa: E731
-            src = ch
-        else:
-            dec_cpu = lambda x: oracle.float_decode(g, 0 if a.kind == "minsum" else 1, I, x,  # noqa: E731
-                                                    early_stop=False, nthreads=nthreads)
-            src = llr
-        host = (lambda S_: src[:, :S_].cpu().numpy().astype(np.int32 if a.kind == "ib" else np.float64))  # noqa: E731
-        S0 = min(16, B)
-        t1 = time.perf_counter()
-        dec_cpu(host(S0))
-        cal = time.perf_counter() - t1
-        S = int(max(S0, min(B, a.cpu_sample, S0 * 12.0 / max(cal, 1e-3))))
-        x_cpu = host(S)
-        t1 = time.perf_counter()
-        ref = dec_cpu(x_cpu)
-        cpu_s = time.perf_counter() - t1
-        if a.kind == "ib":
-            same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int32)))
-            what = (f"oracle/ib_oracle.c (C+OpenMP restatement of the reference OpenCL kernels; the reference's "
-                    f"own numpy host path cannot decode DVB-S2); outputs equal GPU: {same}")
-        else:
-            agree = float(np.mean((ref < 0) == (out[:, :S].cpu().numpy() < 0)))
-            what = (f"oracle/ib_oracle.c fp64 restatement of kernels_min_and_BP.cl (the reference's float host "
-                    f"paths are broken, SURVEY App. C3); hard decisions equal to the GPU's fp32: {agree:.6f}")
-        cpu = {"value": round(S / cpu_s, 3), "unit": "codewords/s", "cores": nthreads, "kind": "port",
-               "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, fixed iterations; {what}; "
-                         f"{cpu_s:.1f} s wall"}
+        cpu = cpu_baseline(a, g, arrays, I, B, match, ch if a.kind == "ib" else llr, out, code_name)
 
     if rank == 0:
         line = {
@@ -272,24 +419,7 @@ def main():
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
             "hbm_gbps_algorithmic": round(value * bpc / 1e9, 1),
             "bytes_per_codeword": bpc,
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "bytes_per_launch": kbytes, "avg_launch_ms": round(kavg, 4),
-                         "stored_format": fmt, "stored_bytes_per_launch": kstored,
-                         "achieved_stored": round(achieved_stored, 1),
-                         "frac_stored": round(achieved_stored / HBM_PEAK_GBPS, 4),
-                         "lds_lookups_per_clk_per_cu": lds,
-                         "note": ("achieved/frac price SURVEY §8(d)'s u8 messages; this build stores 4-bit "
-                                  "messages, so the HBM bytes actually moved are achieved_stored/frac_stored "
-                                  "(a u8-equivalent frac above 1 is the nibble format beating the u8 roofline); "
-                                  "the kernel is bound by LDS lookups + VALU issue, see lds_lookups_per_clk_per_cu")
-                         if fmt == "u4" else
-                         ("fused on-chip decoder: every message of a workgroup's codewords stays in LDS for all "
-                          "iterations, so achieved/frac price the algorithmic (HBM-resident design) bytes the kernel "
-                          "avoids; it is bound by LDS/VALU issue, and the HBM bytes it moves are achieved_stored")
-                         if fused else None,
-                         "launches": {"cn": cn_n, "vn": vn_n},
-                         "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "decoded_bit_errors": tot["errors"], "decoded_bits": tot["bits"],
         }

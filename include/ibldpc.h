@@ -185,8 +185,10 @@ void ibl_encoder_destroy(ibl_encoder* h);
 
 /* Random information bits u8 [n][B] (np.random.randint(0, 2, (data_len, msg_at_time)) in
  * LDPC_Transmitter.py:111): bit i = top bit of the i-th 64-bit output of numpy's Philox4x64-10
- * stream with key (seed, 0) advanced by `offset` blocks (Generator(Philox(key=seed)).advance(offset)
- * .random_raw(n*B) >> 63); the next batch uses offset += ceil(n*B/4). */
+ * stream with key (seed, 1) advanced by `offset` blocks
+ * (Generator(Philox(key=seed + 2**64)).advance(offset).random_raw(n*B) >> 63); the next batch uses
+ * offset += ceil(n*B/4). Key word 1 = 1 keeps the information bits disjoint from the channel stream
+ * of ibl_channel_sample, whose key is (seed, 0), for any seed. */
 int ibl_random_bits(uint64_t seed, uint64_t offset, int32_t n, int32_t B, uint8_t* d_out, void* stream);
 
 /* Bit errors of decoder output against transmitted bits: *d_count = #{(r,b): r < rows, b < B,

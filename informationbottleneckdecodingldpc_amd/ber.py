@@ -18,7 +18,8 @@ over ranks (one small all-reduce per ``sync_every`` batches) so every rank stops
 
 ``encoded=True`` transmits random encoded codewords instead (the reference's
 ``LDPC_BPSK_Transmitter`` + encoder path, AWGN_Channel_Transmission/LDPC_Transmitter.py:109-125): bits
-from the device Philox stream (key ``seed + rank``), batched device encoding, the channel mirrored by
+from the device Philox stream (key ``(seed + rank, 1)``, disjoint from the channel's ``(seed + rank, 0)``),
+batched device encoding, the channel mirrored by
 the codeword bits, and decided bits compared with the transmitted ones (``ibl_count_errors``) over the
 rows ``return_errors_all_zero`` counts.
 """

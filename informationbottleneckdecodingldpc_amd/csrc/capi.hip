@@ -517,6 +517,16 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
         (rc = pick_cfg(1, VM, 4 * h->vn_nt, h->vn_ncs, g->num_cus, &h->kvn)) ||
         (rc = pick_cfg(2, VM, 4 * h->dec_nt, 0, g->num_cus, &h->kdec)))
       return bail(rc);
+    // The fast kernels are built to run without a private segment (launch bounds sized to the node
+    // bodies' registers, item buffers forced inline). A build whose compiler spills registers or passes
+    // an item through scratch would silently lose the register budget the design rests on, and such a
+    // build once faulted (DESIGN.md "Private segment"): refuse it loudly instead.
+    size_t priv = 0;
+    const char* kname = "";
+    HIPCHK(ib_fast_private_bytes(CM, VM, &priv, &kname));
+    if (priv != 0 && !getenv("IBL_ALLOW_SCRATCH"))   // diagnostics only (the spill experiment)
+      return bail(fail(IBL_EHIP, std::string("fast-path kernel ") + kname + " has a " + std::to_string(priv) +
+                                     "-byte private segment (register spill / scratch item): rebuild required"));
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
     if ((rc = dupload(&h->cn_lut, cn_lut, cn_len)) || (rc = dupload(&h->vn_lut, vn_lut, vn_len))) return bail(rc);
@@ -810,6 +820,14 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_vn = std::min(bpc, 1024 / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
   if ((rc = fused_setup(h))) return bail(rc);
+  {  // same guard as the IB fast path: the float kernels are built to run without scratch
+    size_t priv = 0;
+    const char* kname = "";
+    HIPCHK(fl_private_bytes(kind, precision, g->dcm, g->dvm, h->fused_ok ? std::max(g->dcm, g->dvm) : 0, &priv, &kname));
+    if (priv != 0)
+      return bail(fail(IBL_EHIP, std::string("float kernel ") + kname + " has a " + std::to_string(priv) +
+                                     "-byte private segment (register spill): rebuild required"));
+  }
   *out = h;
   return IBL_OK;
 }

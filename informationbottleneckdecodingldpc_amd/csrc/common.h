@@ -176,6 +176,9 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
 int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for this max degree
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu);
+// Largest private (scratch) segment over the fast-path kernels a decoder of max degree maxd launches
+// (CN with and without gather, VN, decision); *name receives that kernel's name.
+hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name);
 hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);
@@ -218,6 +221,9 @@ hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid,
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
+// Largest private segment over the float kernels of (kind, prec, degrees); fused included when asked.
+hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, int fused_maxd, size_t* bytes,
+                            const char** name);
 int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
 hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block);

@@ -118,6 +118,8 @@ __global__ void enc_unpack(const uint8_t* __restrict__ info, const uint32_t* __r
 }
 
 // ---------------------------------------------------------------- BER-driver helpers
+constexpr uint64_t kInfoBitsKeyHi = 1;   // Philox key word 1 of the information-bit stream
+
 __device__ __forceinline__ void philox4x64_10_e(uint64_t c[4], uint64_t k0, uint64_t k1) {
   constexpr uint64_t M0 = 0xD2E7470EE14C6C93ull, M1 = 0xCA5A826395121157ull;
   constexpr uint64_t W0 = 0x9E3779B97F4A7C15ull, W1 = 0xBB67AE8584CAA73Bull;
@@ -131,6 +133,10 @@ __device__ __forceinline__ void philox4x64_10_e(uint64_t c[4], uint64_t k0, uint
   }
 }
 
+// Information bits use Philox key (seed, 1); the channel generator (channel_kernels.hip) uses key
+// (seed, 0). The high key word keeps the two streams disjoint for every seed: with one key, the bit
+// at a position would be the top bit of the very output whose mantissa is the channel uniform there,
+// and the noise would depend on the transmitted bit.
 __global__ void random_bits(uint64_t seed, uint64_t offset, int64_t total, uint8_t* out) {
   const int64_t nblk = (total + 3) / 4;
   for (int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; blk < nblk; blk += (int64_t)gridDim.x * blockDim.x) {
@@ -138,7 +144,7 @@ __global__ void random_bits(uint64_t seed, uint64_t offset, int64_t total, uint8
     const uint64_t add = (uint64_t)blk + 1;
     c[0] += add;
     if (c[0] < add) c[1] = 1;
-    philox4x64_10_e(c, seed, 0);
+    philox4x64_10_e(c, seed, kInfoBitsKeyHi);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int64_t i = blk * 4 + s;

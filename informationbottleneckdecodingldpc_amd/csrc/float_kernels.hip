@@ -749,6 +749,26 @@ hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) 
   return hipGetLastError();
 }
 
+hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, int fused_maxd, size_t* bytes,
+                            const char** name) {
+  const struct { const void* f; const char* n; } ks[] = {
+      {fl_kernel(0, kind, prec, cn_maxd), "fl_cn"}, {fl_kernel(1, kind, prec, vn_maxd), "fl_vn"},
+      {fused_maxd > 0 ? fl_fused_kernel(kind, prec, fused_maxd) : nullptr, "fl_fused"}};
+  *bytes = 0;
+  *name = "";
+  for (const auto& k : ks) {
+    if (!k.f) continue;
+    hipFuncAttributes fa;
+    const hipError_t e = hipFuncGetAttributes(&fa, k.f);
+    if (e != hipSuccess) return e;
+    if (fa.localSizeBytes > *bytes) {
+      *bytes = fa.localSizeBytes;
+      *name = k.n;
+    }
+  }
+  return hipSuccess;
+}
+
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fl_kernel(which, kind, prec, maxd),
                                                       fl_block(which, kind, prec, maxd), 0);

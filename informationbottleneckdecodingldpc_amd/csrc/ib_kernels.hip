@@ -250,14 +250,18 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
     // its bit 3 iff m >= T/2 without a carry into the next nibble (m < T <= 16), so the XOR of the
     // D biased words holds in bit 3 of nibble k the parity of (m >= T/2) of codeword k; the parity
     // of (m < T/2) is that XOR (D & 1).
+    // The wave's verdict is kept wave-uniform (one ballot per item, SGPRs) rather than as a per-lane
+    // flag live across the whole pass.
     const uint32_t bias = (uint32_t)(8 - a.half) * 0x11111111u;
+    uint32_t any = 0;
 #pragma unroll
     for (int i = 0; i < W; ++i) {
       uint32_t x = (D & 1) ? 0x88888888u : 0u;
 #pragma unroll
       for (int j = 0; j < D; ++j) x ^= b.row[j][i] + bias;
-      if (x & 0x88888888u & valid_nib8(a.B - b.cwb - 8 * i)) unsat = true;
+      any |= x & 0x88888888u & valid_nib8(a.B - b.cwb - 8 * i);
     }
+    if (__ballot(any != 0) != 0ull) unsat = true;
   }
 #pragma unroll
   for (int i = 0; i < W; ++i) {
@@ -408,7 +412,8 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 // (a degree-2 node then issues 4 row loads, not MAXD).
 template <class Buf, bool VN, bool GATHER, int DLO>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
-                                         int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat, int& items_done) {
+                                         int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat,
+                                         uint64_t* trace_items) {
   // always inlined: an out-of-line body would take the item by reference through scratch
   auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
     settle(cur);
@@ -462,7 +467,8 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     if (next >= end) break;
     item = next;
   }
-  items_done += done;
+  // trace word {items | cu << 32}: accumulated in memory, not in a register live across the passes
+  if (trace_items && lane == 0) *trace_items += (uint64_t)done;
 }
 
 template <int MAXD, bool VN, bool GATHER>
@@ -473,14 +479,19 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
   const int heavy_end = a.n_heavy * a.nchunks, nitems = a.n_nodes * a.nchunks;
-  const bool do_par = !VN && a.unsat != nullptr;
+  const bool do_par = !VN && !GATHER && a.unsat != nullptr;   // pass 0 (gather) has no syndrome
   bool unsat = false;
   constexpr int W = rowW<MAXD>();
-  const uint64_t t0 = a.trace ? __builtin_readcyclecounter() : 0;
+  // trace words written as they arise (start clock, items): values live across the whole pass cost
+  // the MAXD=8 check node 2 spilled VGPRs
+  uint64_t* trace_items = a.trace ? a.trace + 3 * gw + 2 : nullptr;
+  if (a.trace && lane == 0) {
+    a.trace[3 * gw] = __builtin_readcyclecounter();
+    *trace_items = (uint64_t)__smid() << 32;
+  }
   int* ctr = lds_counters(lds, a);  // 2 phase counters
   // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
   const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)a.nt * kRegion;
-  int mine = 0;
   // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
   // degree-2/3 variables, few lookups per byte moved) by HBM. Waves whose index / 4 in the block is
   // below IBL_MIX take the light share first, so both kinds run side by side on every CU; a wave that
@@ -490,31 +501,33 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)
       ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
-                                                      mine);
+                                                      trace_items);
     else
       ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
-                                                   unsat, mine);
+                                                   unsat, trace_items);
   }
   if (a.trace && lane == 0) {
-    const uint64_t t1 = __builtin_readcyclecounter();
-    a.trace[3 * gw] = t0;
-    a.trace[3 * gw + 1] = t1;
-    a.trace[3 * gw + 2] = (uint64_t)mine | ((uint64_t)__smid() << 32);
+    a.trace[3 * gw + 1] = __builtin_readcyclecounter();
   }
-  if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
+  if (do_par && unsat && lane == 0) atomicOr(&a.unsat[gw & (kShards - 1)], 1);
 }
 
 // MAXD=16 bodies need more than the 128 VGPRs a 1024-thread block allows: cap those at 512
 // threads (256 VGPRs, no scratch spill); the MAXD=8 bodies fit 1024-thread blocks at W <= 2.
+// (IBL_LB16 exists for the spill experiment of DESIGN.md "Private segment"; ibl_ib_create refuses
+// a build whose fast kernels have a private segment.)
 #ifndef IBL_LB8
 #define IBL_LB8 1024
+#endif
+#ifndef IBL_LB16
+#define IBL_LB16 512
 #endif
 // minimum waves per SIMD for the MAXD=8 bodies (register budget 512 / waves); 1 = no constraint
 #ifndef IBL_WPE8
 #define IBL_WPE8 1
 #endif
 template <int MAXD, bool GATHER>
-__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : IBL_LB16, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
@@ -524,7 +537,7 @@ __global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1
 }
 
 template <int MAXD>
-__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : 512, MAXD <= 8 ? IBL_WPE8 : 1) void ib_vn_fast(IbFastArgs a) {
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : IBL_LB16, MAXD <= 8 ? IBL_WPE8 : 1) void ib_vn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;
   lds_at_zero(lds);
@@ -801,6 +814,26 @@ hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* bl
   if (e != hipSuccess) return e;
   if (block > fa.maxThreadsPerBlock) return hipErrorInvalidValue;  // above the kernel's launch bounds
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, block, lds);
+}
+hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
+  const bool c8 = cn_maxd <= 8, v8 = vn_maxd <= 8;
+  const struct { const void* f; const char* n; } ks[] = {
+      {c8 ? (const void*)ib_cn_fast<8, true> : (const void*)ib_cn_fast<16, true>, c8 ? "ib_cn_fast<8,gather>" : "ib_cn_fast<16,gather>"},
+      {c8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>, c8 ? "ib_cn_fast<8>" : "ib_cn_fast<16>"},
+      {v8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>, v8 ? "ib_vn_fast<8>" : "ib_vn_fast<16>"},
+      {(const void*)ib_dec_fast, "ib_dec_fast"}};
+  *bytes = 0;
+  *name = "";
+  for (const auto& k : ks) {
+    hipFuncAttributes fa;
+    const hipError_t e = hipFuncGetAttributes(&fa, k.f);
+    if (e != hipSuccess) return e;
+    if (fa.localSizeBytes > *bytes) {
+      *bytes = fa.localSizeBytes;
+      *name = k.n;
+    }
+  }
+  return hipSuccess;
 }
 static int gen_grid(int n_nodes, int B) {
   const long long items = (long long)n_nodes * ((B + 255) / 256);

@@ -174,7 +174,11 @@ class FloatDecoder:
         _check_tensor(out, self.device, n, "output")
         if out.dtype not in _DT_FL or out.shape[1] != B:
             raise ValueError("output must be float32/float64 [N][B]")
-        it_ptr = iters.data_ptr() if iters is not None else None
+        it_ptr = None
+        if iters is not None:
+            if iters.dtype != torch.int32 or iters.device != self.device or iters.numel() < 1:
+                raise ValueError("iters must be an int32 device tensor")
+            it_ptr = iters.data_ptr()
         _lib.check(_lib.load().ibl_float_decode(self._h, llr.data_ptr(), _DT_FL[llr.dtype], B, out.data_ptr(),
                                                 _DT_FL[out.dtype], int(bool(early_stop)), it_ptr,
                                                 _stream_ptr(self.device)), "ibl_float_decode")

@@ -66,8 +66,9 @@ class LDPCEncoder:
 
 class LDPC_BPSK_Transmitter:
     """Random information words, encoded and BPSK-mapped (0 -> +1, 1 -> -1), ``msg_at_time`` per call
-    (LDPC_Transmitter.py:16-133). Bits come from the numpy-compatible Philox stream (key ``seed``,
-    counter ``offset``, advanced by each call) instead of numpy's global ``randint``.
+    (LDPC_Transmitter.py:16-133). Bits come from the numpy-compatible Philox stream (key
+    ``(seed, 1)`` — disjoint from the channel generator's ``(seed, 0)`` — counter ``offset``, advanced by
+    each call) instead of numpy's global ``randint``.
 
     ``transmit()`` returns host float64 [N][msg_at_time] symbols like the reference;
     ``transmit_bits()`` keeps everything on the device and returns the u8 [N][B] codeword bits (the

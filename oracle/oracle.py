@@ -32,7 +32,7 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(_HERE, f) for f in ("ib_oracle.c", "channel_oracle.c")]
+        srcs = [os.path.join(_HERE, f) for f in ("ib_oracle.c", "float_oracle.inc", "channel_oracle.c", "Makefile")]
         if not os.path.exists(_LIB_PATH) or any(
                 os.path.exists(src) and os.path.getmtime(src) > os.path.getmtime(_LIB_PATH) for src in srcs):
             build()
@@ -46,6 +46,11 @@ def lib():
         L.ibo_float_decode.argtypes = [i32, i32, i64, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p,
                                        i32, i32, ctypes.c_double, _f64p, i32, i32, _f64p,
                                        ctypes.POINTER(i32), i32]
+        _f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+        L.ibo_float32_decode.restype = ctypes.c_int
+        L.ibo_float32_decode.argtypes = [i32, i32, i64, _i32p, _i32p, _i32p, _i32p, _i32p, _i32p,
+                                         i32, i32, ctypes.c_float, _f32p, i32, i32, _f32p,
+                                         ctypes.POINTER(i32), ctypes.c_void_p, i32]
         L.ibo_max_threads.restype = ctypes.c_int
         for nm in ("ibo_minsum_fold", "ibo_vn_sum"):
             getattr(L, nm).restype = ctypes.c_double
@@ -107,6 +112,34 @@ def float_decode(g, kind: int, imax: int, llr: np.ndarray, early_stop: bool = Fa
     return (out, iters.value) if return_iters else out
 
 
+def float32_decode(g, imax: int, llr: np.ndarray, early_stop: bool = False, llr_max: float = 150.0,
+                   nthreads: int = 0, return_iters: bool = False, return_syndromes: bool = False):
+    """Oracle fp32 min-sum decode (the exact float32 restatement: same operations in the same order
+    as kernels_min_and_BP.cl, IEEE single arithmetic) of [N][B] float32 LLRs -> [N][B] float32.
+    return_syndromes adds the syndrome sum after every loop iteration (index i = iteration i,
+    -1 where none ran)."""
+    llr = _c(llr, np.float32)
+    if llr.ndim == 1:
+        llr = llr[:, None]
+    N, B = llr.shape
+    out = np.zeros((N, B), dtype=np.float32)
+    iters = ctypes.c_int32(0)
+    syn = np.zeros(max(int(imax), 1), dtype=np.int64)
+    rc = lib().ibo_float32_decode(g.n_v, g.n_c, g.n_e, _c(g.cn_start, np.int32), _c(g.cn_deg, np.int32),
+                                  _c(g.tgt_cn, np.int32), _c(g.vn_start, np.int32), _c(g.vn_deg, np.int32),
+                                  _c(g.tgt_vn, np.int32), MINSUM, int(imax), float(llr_max), llr, B,
+                                  int(bool(early_stop)), out, ctypes.byref(iters),
+                                  syn.ctypes.data if return_syndromes else None, int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"oracle float32_decode failed rc={rc}")
+    res = (out,)
+    if return_iters:
+        res += (iters.value,)
+    if return_syndromes:
+        res += (syn,)
+    return res if len(res) > 1 else out
+
+
 def max_threads() -> int:
     return int(lib().ibo_max_threads())
 
@@ -160,6 +193,8 @@ def channel_sample(cdf: np.ndarray, seed: int, offset: int, n: int, B: int,
 
 def random_bits(seed: int, offset: int, n: int, B: int) -> np.ndarray:
     """u8 [n][B] information bits of ibl_random_bits: top bit of each 64-bit output of numpy's
-    Philox4x64-10 stream with key seed, counter offset (the stand-in for LDPC_Transmitter.py:111's
+    Philox4x64-10 stream with key (seed, 1) — key word 1 set, so the stream is disjoint from the
+    channel's key (seed, 0) — and counter offset (the stand-in for LDPC_Transmitter.py:111's
     np.random.randint(0, 2, (data_len, msg_at_time)))."""
-    return (philox_raw(int(offset), int(seed), int(n) * int(B)) >> np.uint64(63)).astype(np.uint8).reshape(n, B)
+    key = (int(seed) & (2 ** 64 - 1)) | (1 << 64)
+    return (philox_raw(int(offset), key, int(n) * int(B)) >> np.uint64(63)).astype(np.uint8).reshape(n, B)

@@ -103,7 +103,18 @@ def test_wlan_n1944_and_single_word():
 
 @pytest.mark.parametrize("seed,offset,n,B", [(0, 0, 5, 3), (11, 7, 33, 9), (2 ** 40 + 3, 2 ** 33, 8, 4)])
 def test_random_bits_are_top_bits_of_numpy_philox(seed, offset, n, B):
-    g = np.random.Philox(key=seed)
+    g = np.random.Philox(key=seed + 2 ** 64)      # key word 1 = 1: the information-bit stream
     g.advance(offset)
     ref = (g.random_raw(n * B) >> np.uint64(63)).astype(np.uint8).reshape(n, B)
     np.testing.assert_array_equal(oracle.random_bits(seed, offset, n, B), ref)
+
+
+def test_random_bits_independent_of_channel_stream():
+    """The encoded BER mode draws bits and channel uniforms with the same seed and counter origin; the
+    two Philox keys differ in word 1, so a bit is not the top bit of the uniform that perturbs it
+    (with one key, u >= 0.5 exactly where bit = 1). Channel uniform at position i: output i >> 11."""
+    n, B = 64, 512
+    bits = oracle.random_bits(3, 0, n, B).reshape(-1)
+    u_top = (oracle.philox_raw(0, 3, n * B) >> np.uint64(63)).astype(np.uint8)
+    agree = float(np.mean(bits == u_top))
+    assert abs(agree - 0.5) < 4 * 0.5 / np.sqrt(n * B), agree

@@ -147,3 +147,29 @@ def test_dropin_classes_setup_without_gpu(wlan_H, dvb_H):
         d.decode_OpenCL(np.zeros((64800, 2), dtype=np.int32))
     with pytest.raises(RuntimeError, match="no HIP device"):
         bp.decode_OpenCL_belief_propagation(np.zeros((1296, 4)))
+
+
+def test_decode_kernels_have_no_private_segment(lib):
+    """Every decode kernel of the built library runs without scratch (no register spill, no item
+    passed through private memory): the code object's metadata says private_segment_fixed_size 0.
+    ibl_ib_create / ibl_float_create check the same at run time (hipFuncGetAttributes) and refuse
+    a build that violates it (DESIGN.md "Private segment")."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import subprocess
+    import tempfile
+    from kstats import code_objects
+    seen = {}
+    for co in code_objects(lib.LIB_PATH):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            txt = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name],
+                                 capture_output=True, text=True).stdout
+        for blk in re.split(r"\n\s+- \.", txt):
+            m = re.search(r"\.name:\s+(\S+)", blk)
+            p = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+            if m and p and re.search(r"(ib|fl)_(cn|vn|dec|fused)", m.group(1)):
+                seen[m.group(1)] = int(p.group(1))
+    assert len(seen) >= 20, seen
+    assert {k: v for k, v in seen.items() if v} == {}

@@ -104,3 +104,30 @@ def test_llr_tables_decode_on_oracle(wlan_H):
     ch = q.sample_all_zero(g.n_v, 8, np.random.default_rng(5))
     out = oracle.ib_decode(g, tb, ch, match=True, early_stop=True)
     assert (out[:g.data_len] < 8).sum() == 0
+
+
+@pytest.mark.parametrize("name", ["reg", "wlan"])
+@pytest.mark.parametrize("imax", [1, 2, 10])
+def test_numpy_host_decoder_equals_reference_decode_on_host(golden, reg_H, wlan_H, name, imax):
+    """oracle/host_numpy.py (the C1 CPU baseline: decode_on_host restated in numpy) == the reference's
+    own decode_on_host outputs, regular and irregular class, codeword by codeword."""
+    from oracle.host_numpy import HostDecoder
+    g = graph.build_graph(reg_H if name == "reg" else wlan_H)
+    z = golden
+    dec = HostDecoder(g, 16, 16, imax, z[f"{name}_imax{imax}_cn"], z[f"{name}_imax{imax}_vn"], regular=(name == "reg"))
+    ch = z[f"{name}_imax{imax}_ch"]
+    for k in range(ch.shape[1]):
+        np.testing.assert_array_equal(dec.decode(ch[:, k]), z[f"{name}_imax{imax}_out"][:, k])
+
+
+def test_numpy_host_decoder_equals_oracle_on_c1_code():
+    """C1's regular (3,6) N=8000 code, random tables, i_max=10: the numpy host restatement equals the
+    C oracle (match off, no early stop), which is itself pinned to the reference above."""
+    from oracle.host_numpy import HostDecoder
+    g = graph.build_graph(codes.regular_code(8000, 3, 6, seed=0))
+    tb = tables.random_tables(16, 16, 6, 3, 10, seed=1)
+    ch = np.random.default_rng(2).integers(0, 16, (g.n_v, 3)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=False)
+    dec = HostDecoder(g, 16, 16, 10, tb.cn, tb.vn, regular=True)
+    for k in range(3):
+        np.testing.assert_array_equal(dec.decode(ch[:, k]), ref[:, k])

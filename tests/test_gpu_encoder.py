@@ -150,6 +150,29 @@ def test_dropin_encoder_and_transmitter():
     assert np.array_equal(code.cpu().numpy()[: enc.K], oracle.random_bits(9, engine.philox_blocks(enc.K, 6), enc.K, 6))
 
 
+def test_encoded_channel_noise_independent_of_bits():
+    """Encoded BER mode: raw channel error rates for transmitted 0s and 1s are equal and match the
+    all-zero mode (same seed, same counter origin as run_ber uses for both streams)."""
+    from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+    n, B, seed = 1024, 1024, 3
+    q = UniformQuantizer(sigma2_from_ebn0(1.0, 0.5), 16)
+    bits = torch.empty((n, B), dtype=torch.uint8, device=DEV)
+    engine.random_bits(bits, seed, 0)
+    ch = torch.empty((n, B), dtype=torch.uint8, device=DEV)
+    engine.channel_sample(ch, q.cdf_t_given_x_equals_zero, seed, 0, bits=bits)
+    ch0 = torch.empty((n, B), dtype=torch.uint8, device=DEV)
+    engine.channel_sample(ch0, q.cdf_t_given_x_equals_zero, seed, 0)
+    b = bits.cpu().numpy().astype(bool)
+    decided_one = ch.cpu().numpy() < 8
+    r0 = float(np.mean(decided_one[~b]))            # transmitted 0 decided 1
+    r1 = float(np.mean(~decided_one[b]))            # transmitted 1 decided 0
+    rz = float(np.mean(ch0.cpu().numpy() < 8))
+    p = rz
+    sd = np.sqrt(p * (1 - p) * (1 / (~b).sum() + 1 / b.sum()))
+    assert abs(r0 - r1) < 5 * sd, (r0, r1, rz)
+    assert abs(r0 - rz) < 5 * np.sqrt(p * (1 - p) * 2 / (~b).sum()), (r0, rz)
+
+
 def test_ber_encoded_mode_min_sum():
     from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
     from informationbottleneckdecodingldpc_amd.min_sum_decoder_irreg import Min_Sum_Decoder_class_irregular

@@ -1,17 +1,22 @@
-"""GPU parity of the float min-sum / BP decoders against the fp64 CPU oracle (a restatement of
-kernels_min_and_BP.cl; the reference's own float host path is broken, SURVEY Appendix C3, so
-parity is pinned by the kernel text).
+"""GPU parity of the float min-sum / BP decoders against the CPU oracles (restatements of
+kernels_min_and_BP.cl in fp64 and, for min-sum, fp32; the reference's own float host path is
+broken, SURVEY Appendix C3, so parity is pinned by the kernel text).
 
 Bars (written in the tests):
-  * fp64 min-sum: bit-identical APP LLRs and stop iteration;
+  * fp64 min-sum: bit-identical APP LLRs and stop iteration (vs the fp64 oracle);
   * fp64 BP: |x-y| <= 1e-9 (device exp/log vs glibc differ in the last ulps);
-  * fp32 vs the fp64 oracle (BASELINE: "within 1e-5 relative"): |x-y| <= 1e-5*max(|x|,|y|) +
-    TOL_ABS for >= 99.9 % of APP LLRs and identical hard decisions wherever |oracle LLR| >
-    HARD_EPS — for BP at every i_max tested, for min-sum up to i_max = 10. Unnormalised min-sum
-    on the reference's 16-level quantised LLR alphabet is chaotic past ~20 iterations: sums that
-    cancel exactly to 0 in fp64 (sign() = 0 kills a message) come out as +-1 ulp in fp32, and the
-    trajectories separate (measured: tools/diag_float32.py). There the bar is the decoder's
-    output statistic — the bit-error count — within sampling noise (test_float32_minsum_ber).
+  * fp32 min-sum (BASELINE C3's build): bit-identical APP LLRs and stop iteration vs the fp32
+    oracle — the same selections and ordered adds in IEEE single — at every i_max, including C3's
+    N=1944 / i_max=50, on the per-pass and the fused path;
+  * fp32 min-sum vs the fp64 reference precision: the decoder's error statistic (paired per-codeword
+    bit-error counts) within a stated confidence bound — unnormalised min-sum on the quantised LLR
+    alphabet is chaotic once codewords fail to converge: sums that cancel exactly to 0 in fp64
+    (sign() = 0 kills a message) come out as +-1 ulp in fp32 and the trajectories separate
+    (tools/diag_float32.py);
+  * fp32 BP vs the fp64 oracle: SURVEY H5's |x-y| <= 1e-5*max(|x|,|y|) + 1e-4 on every APP LLR of
+    every codeword the fp64 decoder converges on, identical stop iteration and identical hard
+    decisions wherever the oracle's LLR lies outside that band around 0; on DVB-S2 (C5's code) up to
+    i_max = 100 this holds for every codeword (measured: max |x-y| 4e-4).
 """
 import numpy as np
 import pytest
@@ -20,12 +25,12 @@ import torch
 from informationbottleneckdecodingldpc_amd import graph
 from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
 from oracle import oracle
+from tests._codes import mixed_code
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 REL = 1e-5
-TOL_ABS = {0: 1e-4, 1: 2e-3}      # min-sum: fp32 sums of LLRs; BP: + fp32 log/exp per box-plus
-HARD_EPS = 1e-2
+TOL_ABS = 1e-4                    # |x-y| <= 1e-5*max(|x|,|y|) + 1e-4
 
 
 @pytest.fixture(scope="module")
@@ -69,31 +74,134 @@ def test_float64_vs_oracle(eng, kind, name, imax, B, early, ebn0, path, wlan_H, 
         np.testing.assert_allclose(out, ref, rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("kind,name,imax,B,ebn0", [
-    (oracle.MINSUM, "wlan", 10, 256, 1.5), (oracle.MINSUM, "reg", 10, 70, 2.0), (oracle.MINSUM, "dvb", 10, 8, 1.2),
-    (oracle.BP, "wlan", 10, 256, 1.5), (oracle.BP, "wlan", 50, 100, 2.0), (oracle.BP, "reg", 20, 70, 2.0),
-    (oracle.BP, "dvb", 10, 8, 1.2)])
-def test_float32_vs_oracle(eng, kind, name, imax, B, ebn0, wlan_H, reg_H, dvb_H):
-    g = graph.build_graph({"wlan": wlan_H, "reg": reg_H, "dvb": dvb_H}[name])
-    llr = _llrs(g, B, ebn0, seed=3 * imax + B, quantised=True)
-    ref = oracle.float_decode(g, kind, imax, llr)
-    out, _ = _gpu(eng, g, kind, imax, llr, torch.float32, False)
-    tol = REL * np.maximum(np.abs(out), np.abs(ref)) + TOL_ABS[kind]
-    bad = np.abs(out - ref) > tol
-    assert bad.mean() < 1e-3, f"{bad.sum()} of {bad.size} LLRs outside tolerance"
-    hard_diff = ((out < 0) != (ref < 0)) & (np.abs(ref) > HARD_EPS)
-    assert hard_diff.sum() == 0
+def _h5(out, ref):
+    """Entries outside SURVEY H5's tolerance."""
+    return np.abs(out - ref) > REL * np.maximum(np.abs(out), np.abs(ref)) + TOL_ABS
 
 
-def test_float32_minsum_ber(eng, wlan_H):
-    """i_max = 50 fp32 min-sum: bit-error count vs the fp64 oracle within sampling noise."""
-    g = graph.build_graph(wlan_H)
-    llr = _llrs(g, 400, 2.0, seed=77)
+def _hard_flips(out, ref):
+    """Hard-decision differences where the oracle's LLR lies outside the tolerance band around 0 (a
+    value within the band may take either sign and still meet H5)."""
+    return int((((out < 0) != (ref < 0)) & (np.abs(ref) > REL * np.abs(ref) + TOL_ABS)).sum())
+
+
+def _code_of(name, wlan_H, reg_H, dvb_H):
+    from informationbottleneckdecodingldpc_amd import codes
+    if name == "wlan1944":
+        return codes.wlan_80211n(81)
+    return {"wlan": wlan_H, "reg": reg_H, "dvb": dvb_H}[name]
+
+
+@pytest.mark.parametrize("name,imax,B,early,ebn0", [
+    ("wlan1944", 50, 256, False, 1.0),    # BASELINE C3: N=1944, i_max=50 (non-converging batch)
+    ("wlan1944", 50, 300, True, 3.0),     # C3 code, early stop requested
+    ("wlan1944", 30, 64, True, 4.5),      # batch converges: stop before imax-1
+    ("wlan", 50, 129, True, 2.0),
+    ("reg", 50, 70, False, 2.0),
+    ("dvb", 50, 8, False, 1.0)])
+@pytest.mark.parametrize("path", ["auto", "passes"])
+def test_float32_minsum_bit_exact(eng, name, imax, B, early, ebn0, path, wlan_H, reg_H, dvb_H):
+    """fp32 min-sum == the fp32 oracle bit for bit (selections + ordered IEEE single adds)."""
+    g = graph.build_graph(_code_of(name, wlan_H, reg_H, dvb_H))
+    llr = _llrs(g, B, ebn0, seed=5 * imax + B).astype(np.float32)
+    ref, ref_it = oracle.float32_decode(g, imax, llr, early_stop=early, return_iters=True)
+    out, it = _gpu(eng, g, oracle.MINSUM, imax, llr, torch.float32, early, path=path)
+    assert it == ref_it
+    np.testing.assert_array_equal(out, ref.astype(np.float64))
+
+
+@pytest.mark.parametrize("ebn0", [1.0, 2.0, 3.0])
+def test_float32_minsum_c3_error_statistics(eng, ebn0):
+    """BASELINE C3 (WLAN N=1944 min-sum fp32, i_max=50) vs the reference's fp64 precision on the same
+    channel: the per-codeword bit-error counts d_c = e32_c - e64_c are paired; |mean(d)| must lie
+    within 4 standard errors (two-sided, ~6e-5 false-alarm rate under 'same decoder statistic'), and
+    so must the discordant frame errors (McNemar: |n10 - n01| <= 4 sqrt(n10 + n01))."""
+    from informationbottleneckdecodingldpc_amd import codes
+    g = graph.build_graph(codes.wlan_80211n(81))
+    B = 512
+    llr = _llrs(g, B, ebn0, seed=int(ebn0 * 10))
     ref = oracle.float_decode(g, oracle.MINSUM, 50, llr)
-    out, _ = _gpu(eng, g, oracle.MINSUM, 50, llr, torch.float32, False)
-    e_ref = int((ref[:g.data_len] < 0).sum())
-    e_gpu = int((out[:g.data_len] < 0).sum())
-    assert abs(e_gpu - e_ref) <= max(10, 4 * np.sqrt(e_ref + 1)), (e_gpu, e_ref)
+    out, _ = _gpu(eng, g, oracle.MINSUM, 50, llr.astype(np.float32), torch.float32, False)
+    e64 = (ref[:g.data_len] < 0).sum(0).astype(np.float64)
+    e32 = (out[:g.data_len] < 0).sum(0).astype(np.float64)
+    d = e32 - e64
+    se = d.std(ddof=1) / np.sqrt(B) if B > 1 else 0.0
+    assert abs(d.mean()) <= 4 * se, (d.mean(), se, e32.sum(), e64.sum())
+    n10 = int(((e32 > 0) & (e64 == 0)).sum())
+    n01 = int(((e32 == 0) & (e64 > 0)).sum())
+    assert abs(n10 - n01) <= 4 * np.sqrt(n10 + n01), (n10, n01)
+
+
+@pytest.mark.parametrize("name,imax,B,ebn0", [
+    ("wlan", 10, 256, 1.5), ("wlan", 20, 100, 2.0), ("reg", 20, 70, 2.0), ("dvb", 10, 8, 1.2)])
+def test_float32_bp_vs_oracle(eng, name, imax, B, ebn0, wlan_H, reg_H, dvb_H):
+    g = graph.build_graph(_code_of(name, wlan_H, reg_H, dvb_H))
+    llr = _llrs(g, B, ebn0, seed=3 * imax + B, quantised=True)
+    ref = oracle.float_decode(g, oracle.BP, imax, llr)
+    out, _ = _gpu(eng, g, oracle.BP, imax, llr, torch.float32, False)
+    bad = _h5(out, ref)
+    assert bad.sum() == 0, f"{bad.sum()} of {bad.size} LLRs outside H5, max |x-y| {np.abs(out - ref).max():.3e}"
+    assert _hard_flips(out, ref) == 0
+
+
+@pytest.mark.parametrize("ebn0,early", [(0.6, False), (1.0, True), (1.5, False)])
+def test_float32_bp_c5_dvbs2_imax100(eng, dvb_H, ebn0, early):
+    """BASELINE C5 (DVB-S2 BP fp32, i_max=100) on a small batch vs the fp64 oracle: every APP LLR
+    within H5, identical hard decisions and stop iteration (the fp32 forward-backward check node)."""
+    g = graph.build_graph(dvb_H)
+    llr = _llrs(g, 6, ebn0, seed=int(ebn0 * 100))
+    ref, ref_it = oracle.float_decode(g, oracle.BP, 100, llr, early_stop=early, return_iters=True)
+    out, it = _gpu(eng, g, oracle.BP, 100, llr, torch.float32, early)
+    assert it == ref_it
+    bad = _h5(out, ref)
+    assert bad.sum() == 0, f"{bad.sum()} of {bad.size} LLRs outside H5, max |x-y| {np.abs(out - ref).max():.3e}"
+    assert _hard_flips(out, ref) == 0
+
+
+def test_float32_bp_wlan1944_converged_codewords(eng):
+    """WLAN N=1944 BP fp32 at i_max=50/100: H5 on every codeword the fp64 decoder converges on (zero
+    decided errors for the all-zero word); codewords stuck in a trapping set oscillate and their fp32
+    and fp64 trajectories separate, so for them only the decided-error total is compared."""
+    from informationbottleneckdecodingldpc_amd import codes
+    g = graph.build_graph(codes.wlan_80211n(81))
+    for imax, ebn0 in ((50, 1.5), (100, 2.0)):
+        llr = _llrs(g, 32, ebn0, seed=imax)
+        ref = oracle.float_decode(g, oracle.BP, imax, llr)
+        out, _ = _gpu(eng, g, oracle.BP, imax, llr, torch.float32, False)
+        conv = (ref < 0).sum(0) == 0
+        assert conv.sum() >= 24, conv.sum()
+        bad = _h5(out[:, conv], ref[:, conv])
+        assert bad.sum() == 0, f"{bad.sum()} LLRs of converged codewords outside H5"
+        assert ((out[:, conv] < 0).sum() == 0)
+        e_ref, e_gpu = int((ref[:, ~conv] < 0).sum()), int((out[:, ~conv] < 0).sum())
+        assert abs(e_gpu - e_ref) <= max(10, 4 * np.sqrt(e_ref + 1)), (e_gpu, e_ref)
+
+
+@pytest.mark.parametrize("kind", [oracle.MINSUM, oracle.BP])
+@pytest.mark.parametrize("path", ["auto", "passes"])
+def test_float_mixed_degrees(eng, kind, path):
+    """Every float node body: check degrees 2..16 (incl. degree 2's empty folds and the > 8 immediate-
+    store / MAXD=16 instantiations), variable degrees 1..16; fp64 against the fp64 oracle (min-sum
+    bit-exact, BP 1e-9), fp32 min-sum bit-exact against the fp32 oracle, fp32 BP within H5."""
+    g = graph.build_graph(mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15))
+    assert g.d_c_max == 16 and g.d_v_max == 16
+    imax, B = 6, 260
+    llr = _llrs(g, B, 2.0, seed=kind + 11)
+    G = eng.Graph(g, DEV)
+    ref, ref_it = oracle.float_decode(g, kind, imax, llr, early_stop=True, return_iters=True)
+    out, it = _gpu(eng, g, kind, imax, llr, torch.float64, True, graph_obj=G, path=path)
+    assert it == ref_it
+    if kind == oracle.MINSUM:
+        np.testing.assert_array_equal(out, ref)
+        r32 = oracle.float32_decode(g, imax, llr.astype(np.float32)).astype(np.float64)
+        o32, _ = _gpu(eng, g, kind, imax, llr.astype(np.float32), torch.float32, False, graph_obj=G, path=path)
+        np.testing.assert_array_equal(o32, r32)
+    else:
+        np.testing.assert_allclose(out, ref, rtol=0, atol=1e-9)
+        ref_f = oracle.float_decode(g, kind, imax, llr)
+        o32, _ = _gpu(eng, g, kind, imax, llr, torch.float32, False, graph_obj=G, path=path)
+        assert _h5(o32, ref_f).sum() == 0
+        assert _hard_flips(o32, ref_f) == 0
 
 
 def test_imax1_outputs_channel(eng, wlan_H):

@@ -16,6 +16,9 @@ VARIANTS = {
     "w2b": ["IBL_W=2", "IBL_LB8=512"],
     "wpe5": ["IBL_WPE8=5"],
     "wpe6": ["IBL_WPE8=6"],
+    # spill experiment (DESIGN.md "Private segment"): MAXD=16 kernels at 1024-thread launch bounds
+    # (128 VGPRs) spill their item buffers to scratch; run with IBL_ALLOW_SCRATCH=1
+    "spill16": ["IBL_LB16=1024"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
     # Measured on DVB-S2 (B=8192, i_max=50): nc00 170.9k cw/s (CN 0.464 / VN 0.478 ms), nc23 140.9k
     # (0.622 / 0.526), nc22 142.0k, nc33 132.3k, s2 156.5k -> the default build keeps NC = 0.
