@@ -265,9 +265,11 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
     if a.kind == "ib":
         tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
         dec_cpu = lambda x: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nthreads)  # noqa: E731
+    elif a.kind == "minsum":
+        # fp32 min-sum restated in IEEE single (oracle/float_oracle.inc): the same arithmetic as the GPU
+        dec_cpu = lambda x: oracle.float32_decode(g, I, x.astype(np.float32), nthreads=nthreads)  # noqa: E731
     else:
-        dec_cpu = lambda x: oracle.float_decode(g, 0 if a.kind == "minsum" else 1, I, x,  # noqa: E731
-                                                early_stop=False, nthreads=nthreads)
+        dec_cpu = lambda x: oracle.float_decode(g, 1, I, x, early_stop=False, nthreads=nthreads)  # noqa: E731
     S0 = min(16, B)
     t1 = time.perf_counter()
     dec_cpu(host(S0))
@@ -281,10 +283,18 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
         same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int32)))
         what = (f"oracle/ib_oracle.c (C+OpenMP restatement of the reference OpenCL kernels; the reference's "
                 f"own numpy host path cannot decode this code or has no matching); outputs equal GPU: {same}")
+    elif a.kind == "minsum":
+        same = bool(np.array_equal(ref, out[:, :S].cpu().numpy()))
+        what = (f"oracle/ib_oracle.c fp32 restatement of kernels_min_and_BP.cl's min-sum (the reference's float "
+                f"host paths are broken, SURVEY App. C3); APP LLRs equal GPU bit for bit: {same}")
     else:
-        agree = float(np.mean((ref < 0) == (out[:, :S].cpu().numpy() < 0)))
+        o = out[:, :S].cpu().numpy().astype(np.float64)
+        tol = 1e-5 * np.maximum(np.abs(o), np.abs(ref)) + 1e-4
+        within = float(np.mean(np.abs(o - ref) <= tol))
+        agree = float(np.mean((ref < 0) == (o < 0)))
         what = (f"oracle/ib_oracle.c fp64 restatement of kernels_min_and_BP.cl (the reference's float host "
-                f"paths are broken, SURVEY App. C3); hard decisions equal to the GPU's fp32: {agree:.6f}")
+                f"paths are broken, SURVEY App. C3); GPU fp32 APP LLRs within 1e-5 rel + 1e-4: {within:.6f}, "
+                f"hard decisions equal: {agree:.6f}")
     return {"value": round(S / cpu_s, 3), "unit": "codewords/s", "cores": nthreads, "kind": "port",
             "cpu_model": _cpu_model(), "host_cpus": ncpu,
             "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, fixed iterations; {what}; "

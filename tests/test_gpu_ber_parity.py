@@ -1,0 +1,106 @@
+"""BER-curve parity (north_star: "BER curves matching the reference path at every Eb/N0 point").
+
+The BER driver (``ber.run_ber``: the Eb/N0 state machine of ``DVB-S2/BER_simulation_OpenCL.py:101-143``,
+device channel generation, the drop-in decoder with its batch-global early stop,
+``return_errors_all_zero``) is replayed on the CPU: the same state machine over the identical Philox
+channel stream (``oracle.channel_sample``), decoded by the oracle (``oracle.ib_decode`` /
+``oracle.float32_decode``, early stop on, as ``decode_OpenCL*`` do). Bar: identical Eb/N0 points,
+per-point error and block counts, and BER vectors.
+
+Table values: LLR-quantised tables (``tables.llr_tables``) stand in for the reference's IB-designed
+``.pkl`` tables, which need the absent ``ib_base`` package — parity with the published decoders'
+curves is unpinned; parity here is HIP path vs oracle on the same tables and channel.
+"""
+import numpy as np
+import pytest
+import torch
+
+from informationbottleneckdecodingldpc_amd import codes, engine, graph, tables
+from informationbottleneckdecodingldpc_amd.awgn_quantizer import AWGN_Channel_Quantizer
+from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _quanti(cfg, s2):
+    return AWGN_Channel_Quantizer(s2, cfg.AD_max_abs, cfg.cardinality_T_channel, cfg.cardinality_Y_channel)
+
+
+def _replay(cfg, n_v, data_len, R_c, decode, errors_of):
+    """run_ber's state machine (ber.py, reference :101-173) with the oracle as the decoder."""
+    ebn0, ber, errs, blks = [float(cfg.EbN0_dB_start)], [0.0], [], []
+    offset = 0
+    while True:
+        s2 = 10 ** (-ebn0[-1] / 10) / (2 * R_c)
+        q = _quanti(cfg, s2)
+        errors, blocks = 0.0, 0
+        while errors < cfg.min_errors and (cfg.max_blocks is None or blocks < cfg.max_blocks):
+            cl = oracle.channel_sample(q.cdf_t_given_x_equals_zero, cfg.seed, offset, n_v, cfg.msg_at_time)
+            offset += engine.philox_blocks(n_v, cfg.msg_at_time)
+            errors += errors_of(decode(cl, q), data_len)
+            blocks += cfg.msg_at_time
+        ber[-1] = errors / (R_c * blocks * n_v)
+        errs.append(errors)
+        blks.append(blocks)
+        if ber[-1] > cfg.target_error_rate and ebn0[-1] < cfg.EbN0_dB_max_value:
+            step = cfg.EbN0_dB_small_stepwidth if ber[-1] < cfg.BER_go_on_in_smaller_steps \
+                else cfg.EbN0_dB_normal_stepwidth
+            ebn0.append(ebn0[-1] + step)
+            ber.append(0.0)
+        else:
+            break
+    return np.asarray(ebn0), np.asarray(ber), errs, blks
+
+
+def _assert_same(r, ref):
+    ebn0, ber, errs, blks = ref
+    np.testing.assert_allclose(r.EbN0_dB_vector, ebn0, rtol=0, atol=1e-12)
+    assert [int(e) for e in r.errors] == [int(e) for e in errs]
+    assert r.blocks == blks
+    np.testing.assert_array_equal(r.BER_vector, ber)
+    assert len(ebn0) >= 3
+
+
+@pytest.mark.parametrize("name,imax,B,max_blocks,start,stop,step", [
+    ("wlan", 20, 256, 1024, 0.5, 2.0, 0.5),           # WLAN N=1296 (the reference's own generator)
+    ("dvbs2", 20, 32, 64, 1.0, 2.0, 0.5),             # DVB-S2 N=64800, small batches
+])
+def test_ib_ber_curve_equals_oracle(name, imax, B, max_blocks, start, stop, step, wlan_H, dvb_H):
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+        Discrete_LDPC_Decoder_class_irregular
+    H = wlan_H if name == "wlan" else dvb_H
+    g = graph.build_graph(H)
+    cfg = BERConfig(EbN0_dB_start=start, EbN0_dB_max_value=stop, EbN0_dB_normal_stepwidth=step,
+                    EbN0_dB_small_stepwidth=step / 2, target_error_rate=1e-9, min_errors=10 ** 9,
+                    msg_at_time=B, max_blocks=max_blocks, seed=11)
+    design = _quanti(cfg, 10 ** (-1.5 / 10) / (2 * g.R_c))       # tables designed at 1.5 dB
+    tb = tables.llr_tables(design.output_LLRs, g.d_c_max, g.d_v_max, imax)
+    dec = Discrete_LDPC_Decoder_class_irregular(H, imax, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
+                                                match="true")
+    r = run_ber(dec, cfg)
+    ref = _replay(cfg, g.n_v, dec.data_len, float(dec.R_c),
+                  lambda cl, q: oracle.ib_decode(g, tb, cl, match=True, early_stop=True),
+                  lambda out, dl: float((out[:dl] < 8).sum()))
+    _assert_same(r, ref)
+    assert ref[2][0] > ref[2][-1]          # the curve falls over the sweep
+
+
+def test_minsum_fp32_ber_curve_equals_oracle():
+    """BASELINE C3's code and decoder (WLAN N=1944, min-sum fp32, fused on-chip path) with the
+    channel's float32 cluster LLRs: the BER curve equals the fp32 oracle's."""
+    from informationbottleneckdecodingldpc_amd.min_sum_decoder_irreg import Min_Sum_Decoder_class_irregular
+    H = codes.wlan_80211n(81)
+    g = graph.build_graph(H)
+    B = 512
+    dec = Min_Sum_Decoder_class_irregular(H, 30, 16, B)
+    cfg = BERConfig(EbN0_dB_start=1.0, EbN0_dB_max_value=3.0, EbN0_dB_normal_stepwidth=1.0,
+                    EbN0_dB_small_stepwidth=0.5, target_error_rate=1e-9, min_errors=10 ** 9, msg_at_time=B,
+                    max_blocks=1024, seed=5, llr_dtype=torch.float32)
+    r = run_ber(dec, cfg)
+
+    def decode(cl, q):
+        llr = q.output_LLRs.astype(np.float32)[cl]
+        return oracle.float32_decode(g, 30, llr, early_stop=True)
+    ref = _replay(cfg, g.n_v, dec.data_len, float(dec.R_c), decode, lambda out, dl: float((out[:dl] < 0).sum()))
+    _assert_same(r, ref)

@@ -184,9 +184,53 @@ def test_full_size_dvbs2_properties(eng, dvb_H):
     h1 = dec.decode(ch[:, :B // 2].contiguous(), out_dtype=torch.uint8, early_stop=False).clone()
     h2 = dec.decode(ch[:, B // 2:].contiguous(), out_dtype=torch.uint8, early_stop=False).clone()
     assert torch.equal(torch.cat([h1, h2], 1), o1)
-    cols = [0, 1, 4095, 8191]
+    # 64 columns spread over the batch (every row segment / chunk position class) against the oracle
+    cols = sorted(set([0, 1, 511, 512, 1023, 1024, 4095, 8191] +
+                      list(np.random.default_rng(5).choice(B, 56, replace=False))))
+    assert len(cols) >= 64
     ref = oracle.ib_decode(g, tb, ch[:, cols].cpu().numpy().astype(np.int32), match=True)
     np.testing.assert_array_equal(o1[:, cols].cpu().numpy().astype(np.int32), ref)
+
+
+def test_full_size_dvbs2_early_stop_converging(eng, dvb_H):
+    """BASELINE size (DVB-S2, B=8192, i_max=50) with early stop ON and a batch that converges.
+
+    The stop is batch-global (discrete_LDPC_decoder_irreg.py:310-320: the summed syndrome of the
+    variable-to-check messages of the WHOLE batch must be zero); with random noise one of 8192
+    codewords whose messages keep oscillating is enough to prevent it (tools/diag_early_stop.py: no
+    stop at 2.5-5 dB for B=8192, the oracle agrees on small batches). So the batch is 16 copies of a
+    512-codeword sample that converges (LLR tables, 5 dB, the degree-1 parity bit's channel value set
+    reliable — it is forwarded unchanged, kernels_template_irreg.cl:131-136): the 8192-column decode
+    must stop at the same L as the 512-column one, every copy must decode identically, and 64
+    columns must equal the oracle run for exactly L iterations."""
+    g = graph.build_graph(dvb_H)
+    q = UniformQuantizer(sigma2_from_ebn0(5.0, g.R_c), 16)
+    imax, B, S = 50, 8192, 512
+    tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
+    G = eng.Graph(g, DEV)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(7)
+    base = q.sample_all_zero_device(g.n_v, S, DEV, generator=gen)
+    base[np.flatnonzero(g.vn_deg == 1)] = 15
+    it = torch.zeros(1, dtype=torch.int32, device=DEV)
+    small = eng.IBDecoder(G, tb, True, S).decode(base, out_dtype=torch.uint8, early_stop=True, iters=it).clone()
+    L_small = int(it.item())
+    assert 1 <= L_small < imax - 1, L_small
+    ch = base.repeat(1, B // S).contiguous()
+    out = eng.IBDecoder(G, tb, True, B).decode(ch, out_dtype=torch.uint8, early_stop=True, iters=it)
+    L = int(it.item())
+    assert L == L_small
+    assert torch.equal(out, small.repeat(1, B // S))
+    assert int(eng.count_below(out, g.n_v, 8).item()) == 0
+    cols = sorted(np.random.default_rng(6).choice(B, 64, replace=False))
+    x = ch[:, cols].cpu().numpy().astype(np.int32)
+    tbL = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, L + 1)
+    np.testing.assert_array_equal(tbL.cn, tb.cn[:tbL.cn.size])      # same per-iteration tables
+    np.testing.assert_array_equal(tbL.vn, tb.vn[:tbL.vn.size])
+    ref = oracle.ib_decode(g, tbL, x, match=True, early_stop=False)
+    np.testing.assert_array_equal(out[:, cols].cpu().numpy().astype(np.int32), ref)
+    _, it64 = oracle.ib_decode(g, tb, x, match=True, early_stop=True, return_iters=True)
+    assert it64 <= L
 
 
 def test_full_size_dvbs2_decodes_all_zero(eng, dvb_H):
