@@ -55,8 +55,8 @@ def parse():
     p.add_argument("--config", choices=["C1", "C2", "C3", "C4", "C5"], default=None,
                    help="BASELINE.json config preset (sets --code/--kind/--imax/--batch-per-gpu)")
     p.add_argument("--no-match", action="store_true")
-    p.add_argument("--float-path", choices=["auto", "passes", "fused"], default="auto",
-                   help="float decoders: fused on-chip kernel when the code fits in LDS (auto), or per-pass launches")
+    p.add_argument("--path", "--float-path", dest="path", choices=["auto", "passes", "fused"], default="auto",
+                   help="fused on-chip kernel when the code fits in LDS (auto), or per-pass launches")
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
     p.add_argument("--cpu-procs", type=int, default=0, help="numpy host baseline processes (0 = min(16, host CPUs))")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -120,6 +120,42 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
     79 B/clk/CU, MI355X_MICROARCH.md §LDS), with its HBM bytes (channel in, APP out) reported beside."""
     cn_bytes_u8 = 2 * g.n_e * w * B
     vn_bytes_u8 = (2 * g.n_e * w + n_v * w) * B
+
+    def cn_lk(d):     # table lookups of one check of degree d per codeword (prefix sharing, matching composed)
+        return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
+
+    def vn_lk(d):
+        return 0 if d == 1 else (d - 1) + d * (d - 1) // 2
+    if fused and a.kind == "ib":
+        # fused IB kernel: per 8-codeword group and iteration every check reads and writes its d slot
+        # dwords and makes 8*cn_lk(d) ds_read_u8 lookups, every variable likewise; LDS cycles per
+        # wave-instruction (64 lanes): ds_read_u8 / ds_read_b32 2, ds_write_b32 4 (MI355X_MICROARCH.md
+        # §LDS). achieved/peak = LDS bytes moved (a lookup moves 1 B) over time / at this mix's rate.
+        L = I - 1
+        cd, vd = np.asarray(g.cn_deg, np.int64), np.asarray(g.vn_deg, np.int64)
+        lk_cn = 8 * sum(cn_lk(int(d)) for d in cd)
+        lk_vn = 8 * sum(vn_lk(int(d)) for d in vd)
+        lk_dec = 8 * int(vd.sum())
+        E = int(cd.sum())
+        groups = -(-B // 8)
+        # per group: send (E slot writes), L+1 CN passes, L VN passes, decision (E slot reads)
+        rd_slots = (L + 1) * E + L * E + E
+        wr_slots = E + (L + 1) * E + L * E
+        lookups = (L + 1) * lk_cn + L * lk_vn + lk_dec
+        cyc = groups * (rd_slots * 2 + wr_slots * 4 + lookups * 2) / 64.0        # LDS cycles (chip, summed)
+        byts = groups * (4 * (rd_slots + wr_slots) + lookups)
+        t = cn_avg * 1e-3
+        peak = byts / cyc * NUM_CUS * LDS_CLK_GHZ if cyc else 0.0
+        ach = byts / t / 1e9 if t > 0 else 0.0
+        return {"bound": "lds", "kernel": "ib_fused", "achieved": round(ach, 1), "peak": round(peak, 1),
+                "unit": "GB/s", "frac": round(ach / peak, 4) if peak else 0.0, "traffic": None,
+                "bytes_per_launch": int(byts), "avg_launch_ms": round(cn_avg, 4),
+                "lds_lookups_per_clk_per_cu": round(groups * lookups / t / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2) if t > 0 else 0,
+                "hbm": {"bytes_per_launch": 2 * n_v * B, "peak": HBM_PEAK_GBPS},
+                "note": "fused on-chip IB decoder: 8 codewords per workgroup, 4-bit messages in LDS for all "
+                        "iterations; LDS roofline at this kernel's mix of ds_read_u8 lookups and dword slot "
+                        "reads/writes (MI355X_MICROARCH.md §LDS); lds_lookups_per_clk_per_cu against 32",
+                "launches": {"fused": cn_n}}
     if fused:
         # one launch decodes the whole batch: L = imax-1 check passes, L-1 variable passes (16-B slots,
         # N codewords per slot), plus send (E+N slot writes) and the APP output (E+N slot reads)
@@ -159,13 +195,8 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
             "launches": {"cn": cn_n, "vn": vn_n},
             "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}}
     if fmt == "u4":
-        # table lookups per codeword and pass of the fast path (prefix sharing, matching composed), per CU
-        # and clock at the max clock; the LDS serves at most 32 conflict-free ds_read_u8 lanes/clk/CU
-        def cn_lk(d):
-            return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
-
-        def vn_lk(d):
-            return 0 if d == 1 else (d - 1) + d * (d - 1) // 2
+        # table lookups per codeword and pass of the fast path, per CU and clock at the max clock; the LDS
+        # serves at most 32 conflict-free ds_read_u8 lanes/clk/CU
         lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
         avg = {"cn": cn_avg, "vn": vn_avg}
         roof["lds_lookups_per_clk_per_cu"] = {k: round(lk[k] / (avg[k] * 1e-3) / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2)
@@ -337,7 +368,7 @@ def main():
 
     if a.kind == "ib":
         tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
-        dec = engine.IBDecoder(G, tb, match, B)
+        dec = engine.IBDecoder(G, tb, match, B, path=a.path)
         ch = q.sample_all_zero_device(n_v, B, dev, generator=gen)
         out = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
         run = lambda: dec.decode(ch, out=out, early_stop=False)     # noqa: E731
@@ -346,7 +377,7 @@ def main():
         w, dtype = 1, "u8"
     else:
         kind = 0 if a.kind == "minsum" else 1
-        dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.float_path)
+        dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.path)
         cl = q.sample_all_zero_device(n_v, B, dev, generator=gen, dtype=torch.int64)
         llr = torch.as_tensor(q.output_LLRs, dtype=torch.float32, device=dev)[cl].contiguous()
         out = torch.empty((n_v, B), dtype=torch.float32, device=dev)
@@ -389,7 +420,7 @@ def main():
     value = world * B * a.steps / elapsed
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
-    fused = a.kind != "ib" and dec.fused
+    fused = dec.fused
     fast = a.kind == "ib" and getattr(dec, "fast_path", False)
     # bytes per stored message / channel value as this build moves them: the IB fast path keeps 4-bit
     # nibbles (2 codewords per byte), the generic IB path u8, the float paths fp32
@@ -423,7 +454,8 @@ def main():
             "config": {"workload": f"{code_name}, "
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, "
-                                   f"{('matching ' + ('on' if match else 'off')) if a.kind == 'ib' else ('fused on-chip kernel' if fused else 'per-pass kernels')}"
+                                   f"{('matching ' + ('on' if match else 'off') + ', ') if a.kind == 'ib' else ''}"
+                                   f"{'fused on-chip kernel' if fused else 'per-pass kernels'}"
                                    f", fixed iterations",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},

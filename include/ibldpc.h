@@ -86,6 +86,18 @@ int ibl_ib_create(const ibl_graph* g, int32_t T_ch, int32_t T_dec, int32_t imax,
 /* 1 = LDS fast path, 0 = generic path */
 int ibl_ib_path(const ibl_ib* h);
 /*
+ * Decode path of an IB decoder on the fast path (no reference counterpart; results are identical):
+ *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits (E * 4 bytes of messages
+ *                            for 8 codewords plus the largest pass's table regions <= 160 KiB,
+ *                            check degrees >= 2; e.g. regular (3,6) N=8000, WLAN), else per-pass;
+ *   IBL_PATH_PASSES          one launch per check / variable pass, messages in HBM;
+ *   IBL_PATH_FUSED           the fused kernel (IBL_EUNSUPPORTED if the code does not fit).
+ * ibl_ib_path_in_use reports 1 when decodes run the fused kernel.  With the fused kernel the timing
+ * API reports each fused launch as one check-node launch.
+ */
+int ibl_ib_set_path(ibl_ib* h, int32_t path);
+int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
+/*
  * Decode B codewords.  Replaces decode_OpenCL (discrete_LDPC_decoder_irreg.py:245-341;
  * discrete_LDPC_decoder.py:202-295).
  *   d_ch   [N][B] channel cluster ids (IBL_U8 or IBL_I32), values in [0, T_ch)

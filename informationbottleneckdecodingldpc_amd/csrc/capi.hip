@@ -163,6 +163,13 @@ struct ibl_ib {
   int8_t cn_ccol[kMaxD + 1][4] = {{0}}, vn_ccol[kMaxD + 1][4] = {{0}};
   KCfg kcn, kvn, kdec;
   KTimer timer;
+  // fused on-chip path (IbFusedArgs, short codes): task tables, LDS bytes per workgroup, grid
+  int32_t path = IBL_PATH_AUTO;
+  bool fused_ok = false;
+  int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
+  int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0;
+  size_t f_lds = 0;
+  int f_grid = 0, f_block = 0;
   // generic path
   int32_t *cn_lut = nullptr, *vn_lut = nullptr, *mc = nullptr, *mv = nullptr;
   int64_t cn_len = 0, vn_len = 0, mc_len = 0, mv_len = 0;
@@ -360,6 +367,8 @@ int pick_cfg(int which, int maxd, int nt, int ncs, int num_cus, KCfg* k) {
   return best_waves > 0 ? IBL_OK : fail(IBL_EHIP, "no occupancy for IB kernel (LDS too large?)");
 }
 
+int ib_fused_setup(ibl_ib* h);           // fused on-chip IB decoder (defined with the float one below)
+bool ib_fused_in_use(const ibl_ib* h);
 }  // namespace
 
 extern "C" {
@@ -527,6 +536,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     if (priv != 0 && !getenv("IBL_ALLOW_SCRATCH"))   // diagnostics only (the spill experiment)
       return bail(fail(IBL_EHIP, std::string("fast-path kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill / scratch item): rebuild required"));
+    if ((rc = ib_fused_setup(h))) return bail(rc);
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
     if ((rc = dupload(&h->cn_lut, cn_lut, cn_len)) || (rc = dupload(&h->vn_lut, vn_lut, vn_len))) return bail(rc);
@@ -540,6 +550,23 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
 }
 
 int ibl_ib_path(const ibl_ib* h) { return h && h->fast ? 1 : 0; }
+
+int ibl_ib_set_path(ibl_ib* h, int32_t path) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (path != IBL_PATH_AUTO && path != IBL_PATH_PASSES && path != IBL_PATH_FUSED)
+    return fail(IBL_EINVAL, "path must be IBL_PATH_AUTO, IBL_PATH_PASSES or IBL_PATH_FUSED");
+  if (path == IBL_PATH_FUSED && !h->fused_ok)
+    return fail(IBL_EUNSUPPORTED, "code does not fit the fused IB kernel (fast path, E * 4 B of messages plus the "
+                                  "largest pass's tables within 160 KiB, check degrees >= 2)");
+  h->path = path;
+  return IBL_OK;
+}
+
+int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused) {
+  if (!h || !fused) return fail(IBL_EINVAL, "NULL argument");
+  *fused = ib_fused_in_use(h) ? 1 : 0;
+  return IBL_OK;
+}
 
 int ibl_ib_timing(ibl_ib* h, int32_t enable) {
   if (!h) return fail(IBL_EINVAL, "decoder is NULL");
@@ -566,6 +593,7 @@ void ibl_ib_destroy(ibl_ib* h) {
   dfree(h->cin); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
   dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img); dfree(h->cn_cimg); dfree(h->vn_cimg);
   dfree(h->cn_lut); dfree(h->vn_lut); dfree(h->mc); dfree(h->mv);
+  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
   delete h;
 }
 
@@ -582,6 +610,50 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
   const int I = h->imax;
   const bool early = early_stop != 0 && I > 1;
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
+  if (ib_fused_in_use(h)) {
+    // channel as [group][N] dwords of 8 nibbles (the fused kernel's layout), in the staging buffer
+    uint32_t* chT = reinterpret_cast<uint32_t*>(h->ch8);
+    HIPCHK(launch_ib_stage_t(d_ch, ch_dtype, g->n_v, B, h->f_vn_node, chT, s));
+    IbFusedArgs f{};
+    f.cn_img = h->cn_img; f.vn_img = h->vn_img; f.dec_img = h->dec_img; f.chT = chT;
+    f.cn_task = h->f_cn_task; f.vn_task = h->f_vn_task; f.vn_node = h->f_vn_node; f.vn_slot = h->f_vn_slot;
+    f.out = d_out; f.unsat = early ? h->flags : nullptr; f.dL = nullptr;
+    std::memcpy(f.cn_fslot, h->cn_fslot, sizeof(f.cn_fslot));
+    std::memcpy(f.vn_fslot, h->vn_fslot, sizeof(f.vn_fslot));
+    f.cn_nt = h->cn_nt; f.vn_nt = h->vn_nt; f.dec_nt = h->dec_nt; f.nreg = h->f_nreg;
+    f.n_e = (int32_t)g->n_e; f.n_v = g->n_v; f.n_cn_tasks = h->f_ncn; f.n_vn_tasks = h->f_nvn;
+    f.B = B; f.imax = I; f.half = h->T / 2; f.match = h->match; f.out_dtype = out_dtype;
+    const size_t esz = out_dtype == kU8 ? 1 : 4;
+    f.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
+    f.ngroups = (B + 7) / 8;
+    const int grid = std::min(h->f_grid, f.ngroups);
+    // diagnostics: IBL_TRACE_FUSED=<file> records block 0's clock at every phase boundary of its first group
+    const char* ftrace = getenv("IBL_TRACE_FUSED");
+    const size_t ntr = (size_t)3 * (2 * I + 4);
+    if (ftrace) {
+      HIPCHK(hipMalloc((void**)&f.trace, sizeof(uint64_t) * ntr));
+      HIPCHK(hipMemsetAsync(f.trace, 0, sizeof(uint64_t) * ntr, s));
+    }
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_fused(f, h->CM, h->VM, grid, h->f_block, h->f_lds, s); }));
+    if (ftrace) {
+      std::vector<uint64_t> hv(ntr);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(hv.data(), f.trace, sizeof(uint64_t) * ntr, hipMemcpyDeviceToHost));
+      (void)hipFree(f.trace);
+      f.trace = nullptr;
+      if (FILE* fp = fopen(ftrace, "wb")) {
+        fwrite(hv.data(), sizeof(uint64_t), ntr, fp);
+        fclose(fp);
+      }
+    }
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    if (early) {   // pass 2: re-run the batch to the stop iteration (a no-op when it is imax-1)
+      f.unsat = nullptr;
+      f.dL = h->dL;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_fused(f, h->CM, h->VM, grid, h->f_block, h->f_lds, s); }));
+    }
+    return IBL_OK;
+  }
   if (h->fast) {
     const int ccn = ib_fast_chunk(h->CM), cvn = ib_fast_chunk(h->VM);
     const int ldbb = h->ldb / 2;
@@ -686,6 +758,18 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
 }  // extern "C"
 
 namespace {
+// Task tables of the fused kernels (FlFusedArgs, IbFusedArgs): see below.
+struct FusedTasks {
+  std::vector<int32_t> cn_task, vn_task, vn_node, vn_slot;
+};
+int build_fused_tasks(const ibl_graph* g, FusedTasks* ft);
+int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_task, int32_t** vn_node, int32_t** vn_slot) {
+  int rc;
+  if ((rc = dupload(cn_task, ft.cn_task.data(), ft.cn_task.size())) || (rc = dupload(vn_task, ft.vn_task.data(), ft.vn_task.size())) ||
+      (rc = dupload(vn_node, ft.vn_node.data(), ft.vn_node.size())) || (rc = dupload(vn_slot, ft.vn_slot.data(), ft.vn_slot.size())))
+    return rc;
+  return IBL_OK;
+}
 // Task tables of the fused float kernel (FlFusedArgs). Check nodes sorted by degree (heaviest first,
 // stable) and cut into tasks of up to 64 nodes of one degree; edge k of lane i of a check task gets
 // slot first + k*count + i. Variable nodes likewise; vn_slot maps each variable edge (task-major,
@@ -703,6 +787,27 @@ int fused_setup(ibl_float* h) {
     (void)hipGetLastError();
     return IBL_OK;
   }
+  FusedTasks ft;
+  int rc;
+  if ((rc = build_fused_tasks(g, &ft)) ||
+      (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
+    return rc;
+  const std::vector<int32_t>& cn_task = ft.cn_task;
+  const std::vector<int32_t>& vn_task = ft.vn_task;
+  h->f_ncn = (int32_t)(cn_task.size() / 4);
+  h->f_nvn = (int32_t)(vn_task.size() / 4);
+  h->f_maxd = maxd;
+  h->f_lds = lds;
+  h->f_grid = bpc * g->num_cus;
+  h->fused_ok = true;
+  return IBL_OK;
+}
+
+// Check nodes sorted by degree (heaviest first, stable) and cut into tasks of up to 64 nodes of one
+// degree; edge k of lane i of a check task gets slot first + k*count + i. Variable nodes likewise;
+// vn_slot maps each variable edge (task-major, k*count + i) to the slot of the same edge.
+int build_fused_tasks(const ibl_graph* g, FusedTasks* ft) {
+  const int64_t E = g->n_e;
   std::vector<int32_t> tgt_vn((size_t)E);
   if (hipMemcpy(tgt_vn.data(), g->tgt_vn, sizeof(int32_t) * (size_t)E, hipMemcpyDeviceToHost) != hipSuccess)
     return fail(IBL_EHIP, "hipMemcpy failed");
@@ -718,7 +823,7 @@ int fused_setup(ibl_float* h) {
     return idx;
   };
   const std::vector<int64_t> cst = starts(g->h_cn_deg), vst = starts(g->h_vn_deg);
-  std::vector<int32_t> slot_of((size_t)E), cn_task, vn_task, vn_node, vn_slot;
+  std::vector<int32_t> slot_of((size_t)E);
   {
     const std::vector<int32_t> ord = sorted(g->h_cn_deg);
     int32_t slot = 0;
@@ -726,7 +831,7 @@ int fused_setup(ibl_float* h) {
       const int32_t d = g->h_cn_deg[ord[i]];
       int32_t cnt = 0;
       while (i + cnt < ord.size() && cnt < 64 && g->h_cn_deg[ord[i + cnt]] == d) ++cnt;
-      cn_task.insert(cn_task.end(), {slot, cnt, d, 0});
+      ft->cn_task.insert(ft->cn_task.end(), {slot, cnt, d, 0});
       for (int32_t l = 0; l < cnt; ++l)
         for (int32_t k = 0; k < d; ++k) slot_of[(size_t)cst[ord[i + l]] + k] = slot + k * cnt + l;
       slot += cnt * d;
@@ -740,31 +845,54 @@ int fused_setup(ibl_float* h) {
       const int32_t d = g->h_vn_deg[ord[i]];
       int32_t cnt = 0;
       while (i + cnt < ord.size() && cnt < 64 && g->h_vn_deg[ord[i + cnt]] == d) ++cnt;
-      vn_task.insert(vn_task.end(), {(int32_t)i, cnt, d, sidx});
-      vn_slot.resize((size_t)sidx + (size_t)cnt * d);
+      ft->vn_task.insert(ft->vn_task.end(), {(int32_t)i, cnt, d, sidx});
+      ft->vn_slot.resize((size_t)sidx + (size_t)cnt * d);
       for (int32_t l = 0; l < cnt; ++l) {
         const int32_t v = ord[i + l];
-        vn_node.push_back(v);
-        for (int32_t k = 0; k < d; ++k) vn_slot[(size_t)sidx + k * cnt + l] = slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]];
+        ft->vn_node.push_back(v);
+        for (int32_t k = 0; k < d; ++k) ft->vn_slot[(size_t)sidx + k * cnt + l] = slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]];
       }
       sidx += cnt * d;
       i += cnt;
     }
   }
+  return IBL_OK;
+}
+
+// Fused IB decoder eligibility (fast path, no column images, messages + the largest pass's table
+// regions within the CU's LDS, check degree >= 2, an occupancy of >= 1 block without scratch) and
+// task tables. Leaves fused_ok false when the code does not fit.
+int ib_fused_setup(ibl_ib* h) {
+  const ibl_graph* g = h->g;
+  if (!h->fast || h->cn_ncs || h->vn_ncs || g->n_e == 0) return IBL_OK;
+  int min_dc = 1 << 30;
+  for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
+  if (min_dc < 2) return IBL_OK;
+  const int nreg = std::max(h->cn_nt, std::max(h->vn_nt, h->dec_nt));
+  const size_t lds = (size_t)nreg * (kRegion + 1024) + (size_t)g->n_e * 4 + 16;   // tables, raw images, slots
+  if (lds > (size_t)kLdsBytes) return IBL_OK;
+  int bpc = 0, block = 0;
+  size_t priv = 0;
+  if (ib_fused_occupancy(h->CM, h->VM, lds, &bpc, &block, &priv) != hipSuccess || bpc < 1 || priv != 0) {
+    (void)hipGetLastError();
+    return IBL_OK;
+  }
+  FusedTasks ft;
   int rc;
-  if ((rc = dupload(&h->f_cn_task, cn_task.data(), cn_task.size())) ||
-      (rc = dupload(&h->f_vn_task, vn_task.data(), vn_task.size())) ||
-      (rc = dupload(&h->f_vn_node, vn_node.data(), vn_node.size())) ||
-      (rc = dupload(&h->f_vn_slot, vn_slot.data(), vn_slot.size())))
+  if ((rc = build_fused_tasks(g, &ft)) ||
+      (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
     return rc;
-  h->f_ncn = (int32_t)(cn_task.size() / 4);
-  h->f_nvn = (int32_t)(vn_task.size() / 4);
-  h->f_maxd = maxd;
+  h->f_ncn = (int32_t)(ft.cn_task.size() / 4);
+  h->f_nvn = (int32_t)(ft.vn_task.size() / 4);
+  h->f_nreg = nreg;
   h->f_lds = lds;
+  h->f_block = block;
   h->f_grid = bpc * g->num_cus;
   h->fused_ok = true;
   return IBL_OK;
 }
+
+bool ib_fused_in_use(const ibl_ib* h) { return h->fused_ok && h->path != IBL_PATH_PASSES; }
 }  // namespace
 
 extern "C" {

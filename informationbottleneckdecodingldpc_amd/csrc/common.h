@@ -96,6 +96,30 @@ struct IbDecArgs {
   int32_t out_dtype, nt, n_nodes, nchunks, ldb, B, aligned;
 };
 
+// Fused on-chip IB decoder (short codes): a workgroup decodes 8 codewords at a time (one dword of
+// 4-bit messages per edge slot, codeword c in nibble c & 7) through ALL iterations with the messages
+// in LDS. Edge slots follow the check-node tasks as in FlFusedArgs; the per-pass table images are the
+// per-pass kernels' (staged into the table region at LDS address 0 before every phase).
+struct IbFusedArgs {
+  const uint32_t* cn_img;   // CN tables, pass p = 0..imax-1: cn_nt regions x 256 dwords each
+  const uint32_t* vn_img;   // VN tables, pass k = 0..imax-2
+  const uint32_t* dec_img;  // decision tables, pass k = 0..imax-1
+  const uint32_t* chT;      // channel nibbles, [group][position] dwords (codewords 8*group .. 8*group+7),
+                            // positions in variable-task order (vn_node)
+  const int32_t* cn_task;   // per check task: {first slot, count, degree, 0}
+  const int32_t* vn_task;   // per variable task: {first position, count, degree, first vn_slot index}
+  const int32_t* vn_node;   // variable position -> node
+  const int32_t* vn_slot;   // variable task edge k, lane i at [first + k*count + i] -> message slot
+  void* out;                // user output [N][B] (out_dtype)
+  int32_t* unsat;           // non-null: CN pass j >= 1 ORs "unsatisfied" into unsat[j*kShards + shard]
+  const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
+  int32_t cn_fslot[kMaxD + 1], vn_fslot[kMaxD + 1];
+  int32_t cn_nt, vn_nt, dec_nt, nreg;   // regions per pass image; nreg = table regions reserved in LDS
+  int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, B, imax, half, match, out_dtype, aligned, ngroups;
+  uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED): block 0's clock at every phase boundary of its
+                            // first group, else nullptr
+};
+
 // --------------------------------------------------------------- IB generic path
 // Reference-exact flat-vector indexing (any T_ch, T_dec <= 256, any degree).
 struct IbGenArgs {
@@ -179,6 +203,10 @@ hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* bl
 // Largest private (scratch) segment over the fast-path kernels a decoder of max degree maxd launches
 // (CN with and without gather, VN, decision); *name receives that kernel's name.
 hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name);
+hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT,
+                             hipStream_t s);
+hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, int block, size_t lds, hipStream_t s);
+hipError_t ib_fused_occupancy(int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block, size_t* private_bytes);
 hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);

@@ -391,8 +391,10 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // ---------------------------------------------------------------------- kernels
 #define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
+// Variable-pass co-scheduling (see ib_pass): A/B on DVB-S2 B=8192 (tools/ab.sh, 2 reps each, one box):
+// IBL_MIX 0: VN 0.4825 ms / 170.4k cw/s, 1: 0.4709 / 171.5k, 2: 0.4703 / 171.8k, 3: 0.4782 / 171.1k.
 #ifndef IBL_MIX
-#define IBL_MIX 0
+#define IBL_MIX 2
 #endif
 
 // LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
@@ -493,10 +495,10 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
   const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)a.nt * kRegion;
   // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
-  // degree-2/3 variables, few lookups per byte moved) by HBM. Waves whose index / 4 in the block is
-  // below IBL_MIX take the light share first, so both kinds run side by side on every CU; a wave that
+  // degree-2/3 variables, few lookups per byte moved) by HBM. The first IBL_MIX quarters of the
+  // block's waves take the light share first, so both kinds run side by side on every CU; a wave that
   // exhausts its first share joins the other (two ticket counters).
-  const bool light_first = VN && ((threadIdx.x >> 8) < IBL_MIX);
+  const bool light_first = VN && (int)(threadIdx.x >> 6) * 4 < wpb * IBL_MIX;   // IBL_MIX quarters of the block
 #pragma unroll 1
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)
@@ -571,6 +573,339 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
 #undef X
       default: break;
     }
+  }
+}
+
+// ------------------------------------------------------------- fused on-chip decoder
+// For short codes (E * 4 B of messages plus the largest pass's table regions within the CU's LDS,
+// e.g. regular (3,6) N=8000: 96 KB + 32 KB), one workgroup decodes 8 codewords (a dword of 4-bit
+// messages per edge slot) through ALL iterations without touching HBM for messages: the flooding
+// schedule of decode_OpenCL (discrete_LDPC_decoder_irreg.py:277-333, kernels_template_irreg.cl)
+// as barrier-separated phases over one in-place slot array (a node reads all its inputs before it
+// writes its outputs to the same slots):
+//   send (:13-31); CN pass 0 (checknode_update_iter0 :33-99); for j = 1..L { VN pass j-1 (:103-179);
+//   CN pass j (:181-246) + syndrome of its inputs (:304-326) }; decision with the tables of pass L
+//   (calc_varnode_output :249-302).
+// The node bodies are the per-pass kernels' (cn_word / vn_word on one dword, the same generated fold
+// schedules, the same table images and matching-composed final slots), so outputs equal the per-pass
+// path's bit for bit. Tables are staged into the region at LDS address 0 before every phase (each
+// pass has its own tables). Tasks of up to 64 same-degree nodes (lane = node) are handed to waves by
+// LDS tickets. Early stop is batch-global: pass 1 runs imax-1 iterations and records each CN pass's
+// syndrome in the per-pass path's flag words; finalize_iters turns them into L; pass 2 (dL set)
+// re-runs the batch to L only if L < imax-1.
+template <int D>
+__device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt, int lane, uint32_t lane4,
+                                               const IbFusedArgs& a, bool do_par, uint32_t vmask, bool& unsat) {
+  uint32_t in[D], o[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    in[j] = msg[first + j * cnt + lane];
+    o[j] = 0;
+  }
+  if (do_par) {   // parity of (m < T/2) over the inputs, 8 codewords at once (see cn_compute)
+    const uint32_t bias = (uint32_t)(8 - a.half) * 0x11111111u;
+    uint32_t x = (D & 1) ? 0x88888888u : 0u;
+#pragma unroll
+    for (int j = 0; j < D; ++j) x ^= in[j] + bias;
+    if (x & 0x88888888u & vmask) unsat = true;
+  }
+  const uint32_t fbase = slot_off(a.cn_fslot[D]);
+  if constexpr (D == 2) {
+    if (a.match) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
+          t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
+        }
+        o[0] |= pack4n(t0, g);
+        o[1] |= pack4n(t1, g);
+      }
+    } else {
+      o[0] = in[1];
+      o[1] = in[0];
+    }
+  } else {
+    const uint32_t cb[4] = {0, 0, 0, 0};   // no column-fetched inputs (checked on the host: ncs == 0)
+    cn_word<D>(lane4, in, fbase, cb, o);
+  }
+#pragma unroll
+  for (int j = 0; j < D; ++j) msg[first + j * cnt + lane] = o[j];
+}
+
+// A variable task's inputs, fetched one task ahead (register double buffer, as ib_phase): slot
+// indices of its edges (always MAXD loads, clamped to the degree and to the task's last lane, so
+// the number of outstanding loads is static) and the channel dword of its lane's variable.
+template <int MAXD>
+struct VnTask {
+  int pos, cnt, d, sf;
+  uint32_t chw;
+  int32_t sl[MAXD];
+};
+
+template <int MAXD>
+__device__ __forceinline__ void fetch_vn_task(const IbFusedArgs& a, const uint32_t* chg, int t, int lane,
+                                              VnTask<MAXD>& v) {
+  v.pos = sload(a.vn_task, 4 * t);
+  v.cnt = sload(a.vn_task, 4 * t + 1);
+  v.d = sload(a.vn_task, 4 * t + 2);
+  v.sf = sload(a.vn_task, 4 * t + 3);
+  const int li = min(lane, v.cnt - 1);
+  v.chw = chg[v.pos + li];
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) v.sl[k] = a.vn_slot[v.sf + min(k, v.d - 1) * v.cnt + li];
+}
+
+template <int MAXD>
+__device__ __forceinline__ void settle_vn(const VnTask<MAXD>& v) {
+  asm volatile("" ::"v"(v.chw));
+#pragma unroll
+  for (int k = 0; k < MAXD; ++k) asm volatile("" ::"v"(v.sl[k]));
+}
+
+template <int D, int MAXD>
+__device__ __forceinline__ void fused_vn_dword(uint32_t* msg, const VnTask<MAXD>& v, uint32_t lane4,
+                                               const IbFusedArgs& a) {
+  uint32_t in[D], o[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    in[k] = msg[v.sl[k]];
+    o[k] = 0;
+  }
+  if constexpr (D == 1) {
+    o[0] = v.chw;     // degree 1 forwards the channel value (:131-136)
+  } else {
+    const uint32_t cb[4] = {0, 0, 0, 0};
+    vn_word<D>(lane4, in, v.chw, slot_off(a.vn_fslot[D]), cb, o);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) msg[v.sl[k]] = o[k];
+}
+
+// decision of one variable for 8 codewords: fold of channel and ALL inputs, raw tables V_0..V_{D-1}
+template <int D, int MAXD>
+__device__ __forceinline__ void fused_dec_dword(const uint32_t* msg, const VnTask<MAXD>& v, uint32_t lane4,
+                                                uint32_t (&res)[2]) {
+  uint32_t in[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) in[k] = msg[v.sl[k]];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = 4 * g + s;
+      uint32_t Q = lu((nib(v.chw, k) << 11) + qidx(nib(in[0], k), lane4), 0);
+#pragma unroll
+      for (int l = 1; l < D; ++l) Q = luc(Q, qidx(nib(in[l], k), lane4), slot_off(l));
+      packed |= Q << (8 * s);
+    }
+    res[g] = packed;
+  }
+}
+
+// Table staging: a pass's raw image is 256 dwords per region (each entry byte-packed 4 tables deep);
+// the LDS image replicates every dword over the 32 banks (l32[i] = img[i >> 5]). The next phase's raw
+// dwords are loaded into registers at the START of the current phase (2 per thread), written to a
+// small raw buffer in LDS when the wave's tasks are done, and replicated LDS -> LDS after the phase
+// barrier: the phase boundary pays LDS traffic only, not an L2 round trip.
+constexpr int kPfSrc = 2;
+struct TablePrefetch {
+  uint32_t r[kPfSrc];
+  const uint32_t* img;
+  int nsrc;   // raw dwords (nt * 256)
+  __device__ __forceinline__ void load(const uint32_t* im, int nt) {
+    img = im;
+    nsrc = nt * 256;
+#pragma unroll
+    for (int k = 0; k < kPfSrc; ++k) {
+      const int i = threadIdx.x + k * blockDim.x;
+      r[k] = i < nsrc ? img[i] : 0u;
+    }
+  }
+  // before the phase barrier: this thread's raw dwords into the raw buffer
+  __device__ __forceinline__ void put_raw(uint32_t* raw) const {
+#pragma unroll
+    for (int k = 0; k < kPfSrc; ++k) {
+      const int i = threadIdx.x + k * blockDim.x;
+      if (i < nsrc) raw[i] = r[k];
+    }
+    for (int i = threadIdx.x + kPfSrc * blockDim.x; i < nsrc; i += blockDim.x) raw[i] = img[i];
+  }
+  // after the phase barrier: replicate into the table regions at LDS address 0
+  __device__ __forceinline__ void replicate(uint8_t* lds, const uint32_t* raw) const {
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+    const int n = nsrc * 32;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = raw[i >> 5];
+  }
+};
+
+#ifndef IBL_FUSED_TRACE
+#define IBL_FUSED_TRACE 0
+#endif
+// CMAX / VMAX: largest check / variable degree with a body (the variable tasks' index buffers are
+// VMAX deep: a (3,6)-regular code runs ib_fused<8, 4>)
+template <int CMAX, int VMAX>
+__global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(IbFusedArgs a) {
+  constexpr int MAXD = VMAX;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  lds_at_zero(lds);
+  // LDS: [nreg table regions][raw images, nreg x 1 KiB][E message slots][2 counters]
+  uint32_t* raw = reinterpret_cast<uint32_t*>(lds + (size_t)a.nreg * kRegion);
+  uint32_t* msg = raw + (size_t)a.nreg * 256;
+  int* ctr = reinterpret_cast<int*>(msg + a.n_e);
+  const int lane = threadIdx.x & 63;
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  int L = a.imax - 1;
+  if (a.dL) {
+    L = __builtin_amdgcn_readfirstlane(*a.dL);
+    if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
+  }
+  if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+  __syncthreads();
+  int ph = 0;
+  const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
+  TablePrefetch pf;
+  // end of a phase: the next phase's raw tables into LDS, barrier (every wave done with the old
+  // tables and slots), replication, barrier
+  // phase trace (diagnostic builds only: -DIBL_FUSED_TRACE=1, tools/variants.py ftrace)
+  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && threadIdx.x == 0) ? a.trace : nullptr;
+  auto mark = [&](int k) __attribute__((always_inline)) {
+    if constexpr (IBL_FUSED_TRACE) {
+      if (tr) tr[k] = __builtin_readcyclecounter();
+    }
+  };
+  auto next_phase = [&]() __attribute__((always_inline)) {
+    pf.put_raw(raw);
+    __syncthreads();
+    mark(3 * ph + 1);   // all waves done with the phase
+    pf.replicate(lds, raw);
+    __syncthreads();
+    mark(3 * ph + 2);   // next phase's tables staged
+    ++ph;
+    mark(3 * ph);       // next phase starts
+  };
+  // check tasks: slots are contiguous per task (no index loads)
+  auto cn_phase = [&](bool do_par, uint32_t vmask, bool& unsat) __attribute__((always_inline)) {
+    int* c = ctr + (ph & 1);
+    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    for (;;) {
+      const int t = take_ticket(c, lane);
+      if (t >= a.n_cn_tasks) break;
+      const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
+      if (lane < cnt) {
+        switch (d) {
+#define X(D) case D: if constexpr (D <= CMAX) fused_cn_dword<D>(msg, first, cnt, lane, lane4, a, do_par, vmask, unsat); break;
+          IBL_DEG_CASES(X)
+#undef X
+          default: break;
+        }
+      }
+    }
+  };
+  // variable tasks (send / VN pass / decision): task k+1's indices and channel are fetched before task
+  // k is computed (ping-pong buffers, unconditional clamped prefetch: straight-line waits)
+  auto vn_phase = [&](const uint32_t* chg, auto&& body) __attribute__((always_inline)) {
+    int* c = ctr + (ph & 1);
+    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    const int last = a.n_vn_tasks - 1;
+    VnTask<MAXD> A, Bb;
+    int t = take_ticket(c, lane);
+    if (t > last) return;
+    fetch_vn_task(a, chg, t, lane, A);
+    for (;;) {
+      int tn = take_ticket(c, lane);
+      fetch_vn_task(a, chg, min(tn, last), lane, Bb);
+      settle_vn(A);
+      if (lane < A.cnt) body(A);
+      if (tn > last) break;
+      t = take_ticket(c, lane);
+      fetch_vn_task(a, chg, min(t, last), lane, A);
+      settle_vn(Bb);
+      if (lane < Bb.cnt) body(Bb);
+      if (t > last) break;
+    }
+  };
+  for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+    const uint32_t* chg = a.chT + (size_t)grp * a.n_v;   // channel by variable position (vn_node order)
+    const int cwb = grp * 8;
+    const uint32_t vmask = valid_nib8(a.B - cwb);
+    // send: the channel value to every edge slot of its variable
+    mark(0);
+    pf.load(a.cn_img, a.cn_nt);
+    vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+      for (int k = 0; k < v.d; ++k) msg[a.vn_slot[v.sf + k * v.cnt + lane]] = v.chw;
+    });
+    next_phase();
+    for (int j = 0;; ++j) {
+      // CN pass j (tables staged); prefetch the next phase's tables meanwhile
+      if (j == L) pf.load(a.dec_img + (size_t)L * a.dec_nt * 256, a.dec_nt);
+      else pf.load(a.vn_img + (size_t)j * a.vn_nt * 256, a.vn_nt);
+      const bool do_par = j > 0 && a.unsat != nullptr;
+      bool unsat = false;
+      cn_phase(do_par, vmask, unsat);
+      if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)j * kShards + shard], 1);
+      next_phase();
+      if (j == L) break;
+      pf.load(a.cn_img + (size_t)(j + 1) * a.cn_nt * 256, a.cn_nt);
+      vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+        switch (v.d) {
+          case 1: fused_vn_dword<1, MAXD>(msg, v, lane4, a); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_vn_dword<D, MAXD>(msg, v, lane4, a); break;
+          IBL_DEG_CASES(X)
+#undef X
+          default: break;
+        }
+      });
+      next_phase();
+    }
+    // decision with the tables of pass L (staged), 8 codewords of one variable per lane
+    vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+      uint32_t r[2] = {0u, 0u};
+      switch (v.d) {
+        case 1: fused_dec_dword<1, MAXD>(msg, v, lane4, r); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_dec_dword<D, MAXD>(msg, v, lane4, r); break;
+        IBL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+      const size_t o = (size_t)a.vn_node[v.pos + lane] * a.B + cwb;
+      store4(a.out, a.out_dtype, o, 0, a.B - cwb, a.aligned != 0, r[0]);
+      store4(a.out, a.out_dtype, o, 4, a.B - cwb, a.aligned != 0, r[1]);
+    });
+    __syncthreads();   // every wave done with this group's slots before the next group's send
+    mark(3 * ph + 1);
+    ++ph;
+    tr = nullptr;      // first group only
+  }
+}
+
+// channel staging for the fused decoder: user [N][B] (u8 / i32) -> chT [group][position] dwords of 8
+// nibbles, positions in variable-task order (perm[pos] = node), so a task's lanes read consecutive dwords
+__global__ void ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT) {
+  const int ngroups = (B + 7) >> 3;
+  const size_t total = (size_t)ngroups * n;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i / n);
+    const int v = perm[(int)(i - (size_t)g * n)];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int cw = g * 8 + s;
+      uint32_t x = 0;
+      if (cw < B) {
+        if (dtype == kU8) {
+          x = reinterpret_cast<const uint8_t*>(ch)[(size_t)v * B + cw];
+        } else {
+          const int32_t y = reinterpret_cast<const int32_t*>(ch)[(size_t)v * B + cw];
+          x = (uint32_t)min(max(y, 0), 255);
+        }
+      }
+      packed |= min(x, 15u) << (4 * s);
+    }
+    chT[i] = packed;
   }
 }
 
@@ -834,6 +1169,33 @@ hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const 
     }
   }
   return hipSuccess;
+}
+hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT,
+                             hipStream_t s) {
+  const size_t total = (size_t)((B + 7) >> 3) * n;
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, 16384));
+  hipLaunchKernelGGL(ib_stage_t, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, perm, chT);
+  return hipGetLastError();
+}
+static const void* ib_fused_kernel(int cmax, int vmax) {
+  if (cmax <= 8 && vmax <= 4) return (const void*)ib_fused<8, 4>;
+  if (cmax <= 8 && vmax <= 8) return (const void*)ib_fused<8, 8>;
+  return (const void*)ib_fused<16, 16>;
+}
+hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, int block, size_t lds, hipStream_t s) {
+  IbFusedArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(ib_fused_kernel(cmax, vmax), dim3(grid), dim3(block), p, lds, s);
+}
+hipError_t ib_fused_occupancy(int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block, size_t* private_bytes) {
+  const void* f = ib_fused_kernel(cmax, vmax);
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipFuncAttributes fa;
+  if ((e = hipFuncGetAttributes(&fa, f)) != hipSuccess) return e;
+  *block = cmax <= 8 && vmax <= 8 ? 1024 : 512;
+  *private_bytes = fa.localSizeBytes;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
 }
 static int gen_grid(int n_nodes, int B) {
   const long long items = (long long)n_nodes * ((B + 255) / 256);

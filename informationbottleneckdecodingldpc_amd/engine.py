@@ -75,9 +75,16 @@ class Graph:
 
 
 class IBDecoder:
-    """Information-bottleneck lookup-table decoder (``ibl_ib``) for up to ``max_batch`` codewords."""
+    """Information-bottleneck lookup-table decoder (``ibl_ib``) for up to ``max_batch`` codewords.
 
-    def __init__(self, graph: Graph, tables: IBTables, match: bool, max_batch: int, force_generic: bool = False):
+    ``path`` (fast path only): "auto" (the fused on-chip kernel when the code fits in LDS), "passes"
+    (one launch per check / variable pass) or "fused" (raises when the code does not fit); both give
+    identical results (``ibl_ib_set_path``). ``fused`` tells which one decodes run."""
+
+    _PATHS = {"auto": _lib.IBL_PATH_AUTO, "passes": _lib.IBL_PATH_PASSES, "fused": _lib.IBL_PATH_FUSED}
+
+    def __init__(self, graph: Graph, tables: IBTables, match: bool, max_batch: int, force_generic: bool = False,
+                 path: str = "auto"):
         self.graph = graph
         self.tables = tables
         self.match = bool(match)
@@ -96,6 +103,15 @@ class IBDecoder:
                    "ibl_ib_create")
         self._h = h
         self.fast_path = bool(L.ibl_ib_path(h))
+        if path not in self._PATHS:
+            raise ValueError(f"path must be one of {sorted(self._PATHS)}")
+        _lib.check(L.ibl_ib_set_path(h, self._PATHS[path]), "ibl_ib_set_path")
+
+    @property
+    def fused(self) -> bool:
+        f = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_ib_path_in_use(self._h, ctypes.byref(f)), "ibl_ib_path_in_use")
+        return bool(f.value)
 
     def decode(self, ch: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=torch.int32,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:

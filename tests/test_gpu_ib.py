@@ -25,9 +25,9 @@ def eng():
 
 
 def _run(eng, g_edges, tb, ch, match, early, out_dtype=torch.int32, ch_dtype=torch.int32, force_generic=False,
-         graph_obj=None):
+         graph_obj=None, path="auto"):
     G = graph_obj or eng.Graph(g_edges, DEV)
-    dec = eng.IBDecoder(G, tb, match, max_batch=ch.shape[1], force_generic=force_generic)
+    dec = eng.IBDecoder(G, tb, match, max_batch=ch.shape[1], force_generic=force_generic, path=path)
     it = torch.zeros(1, dtype=torch.int32, device=DEV)
     out = dec.decode(torch.from_numpy(ch).to(DEV).to(ch_dtype).contiguous(), out_dtype=out_dtype,
                      early_stop=early, iters=it)
@@ -53,16 +53,20 @@ def _code(name, wlan_H, reg_H, dvb_H):
 
 
 @pytest.mark.parametrize("name,imax,B,match,early", CASES)
-@pytest.mark.parametrize("generic", [False, True])
-def test_ib_random_tables_vs_oracle(eng, name, imax, B, match, early, generic, wlan_H, reg_H, dvb_H):
+@pytest.mark.parametrize("mode", ["auto", "passes", "generic"])
+def test_ib_random_tables_vs_oracle(eng, name, imax, B, match, early, mode, wlan_H, reg_H, dvb_H):
+    """Every path against the oracle: auto (fused on-chip kernel for WLAN / regular, per-pass for
+    DVB-S2), per-pass fast kernels, generic reference-indexing kernels."""
     g = graph.build_graph(_code(name, wlan_H, reg_H, dvb_H))
     T = 16
     tb = tables.random_tables(T, T, g.d_c_max, g.d_v_max, imax, seed=imax * 7 + B)
     rng = np.random.default_rng(B)
     ch = rng.integers(0, T, (g.n_v, B)).astype(np.int32)
     ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
-    out, it, dec = _run(eng, g, tb, ch, match, early, force_generic=generic)
+    generic = mode == "generic"
+    out, it, dec = _run(eng, g, tb, ch, match, early, force_generic=generic, path="passes" if generic else mode)
     assert dec.fast_path == (not generic)
+    assert dec.fused == (mode == "auto" and name != "dvb")
     assert it == ref_it
     np.testing.assert_array_equal(out, ref)
 
@@ -110,6 +114,57 @@ def test_ib_mixed_degrees_fast_path(eng, match, cdegs, vdegs, fast, early):
     assert dec.fast_path == fast
     assert it == ref_it
     np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("name,imax,B,match,early,ebn0", [
+    ("reg8000", 50, 300, False, False, None),     # BASELINE C1/C2 code, ragged batch
+    ("reg8000", 12, 64, False, True, 3.0),        # converging: stop before imax-1 (pass 2 re-run)
+    ("wlan1944", 20, 1001, True, True, None),     # random tables never converge: one pass
+    ("wlan", 9, 17, True, False, None),
+    ("mixed16", 6, 130, False, True, None),       # every node body (degrees 2..16 / 1..16), MAXD=16
+    ("mixed8", 7, 250, True, True, 4.0)])         # MAXD=8 bodies with matching, converging
+def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn0, wlan_H):
+    """The fused on-chip IB kernel (8 codewords per workgroup in LDS for all iterations) equals the
+    per-pass path and the oracle bit for bit, with the same stop iteration."""
+    H = {"reg8000": lambda: codes.regular_code(8000, 3, 6, seed=0), "wlan1944": lambda: codes.wlan_80211n(81),
+         "wlan": lambda: wlan_H,
+         "mixed16": lambda: _mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15),
+         "mixed8": lambda: _mixed_code(np.array([3, 5, 6, 7, 8]), np.array([2, 3, 5, 6, 7, 8]), 500, seed=5)}[name]()
+    g = graph.build_graph(H)
+    G = eng.Graph(g, DEV)
+    if ebn0 is None:
+        tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=B)
+        ch = np.random.default_rng(B).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    else:
+        q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
+        tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
+        ch = q.sample_all_zero(g.n_v, B, np.random.default_rng(B)).astype(np.int32)
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
+    fo, fit, fdec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="fused", out_dtype=torch.uint8,
+                         ch_dtype=torch.uint8)
+    assert fdec.fused
+    po, pit, pdec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="passes")
+    assert not pdec.fused
+    assert fit == pit == ref_it
+    if name == "reg8000" and early:
+        assert ref_it < imax - 1
+    np.testing.assert_array_equal(fo, ref)
+    np.testing.assert_array_equal(po, ref)
+
+
+def test_ib_fused_path_selection(eng, wlan_H, dvb_H):
+    g = graph.build_graph(wlan_H)
+    G = eng.Graph(g, DEV)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 5)
+    assert eng.IBDecoder(G, tb, True, 64).fused
+    assert not eng.IBDecoder(G, tb, True, 64, path="passes").fused
+    assert not eng.IBDecoder(G, tb, True, 64, force_generic=True).fused
+    D = eng.Graph(graph.build_graph(dvb_H), DEV)
+    tbd = tables.random_tables(16, 16, 7, 8, 5)
+    assert not eng.IBDecoder(D, tbd, True, 64).fused         # E * 4 B = 907 KB of messages
+    from informationbottleneckdecodingldpc_amd._lib import IBLError
+    with pytest.raises(IBLError):
+        eng.IBDecoder(D, tbd, True, 64, path="fused")
 
 
 def test_ib_early_stop_converging(eng, wlan_H):

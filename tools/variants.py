@@ -19,6 +19,13 @@ VARIANTS = {
     # spill experiment (DESIGN.md "Private segment"): MAXD=16 kernels at 1024-thread launch bounds
     # (128 VGPRs) spill their item buffers to scratch; run with IBL_ALLOW_SCRATCH=1
     "spill16": ["IBL_LB16=1024"],
+    # variable pass co-scheduling: waves with (threadIdx.x >> 8) < IBL_MIX take the light (degree <= 4,
+    # HBM-bound) items first, the others the heavy (LDS-bound) ones
+    "mix1": ["IBL_MIX=1"],
+    "mix2": ["IBL_MIX=2"],
+    "mix3": ["IBL_MIX=3"],
+    # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
+    "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
     # Measured on DVB-S2 (B=8192, i_max=50): nc00 170.9k cw/s (CN 0.464 / VN 0.478 ms), nc23 140.9k
     # (0.622 / 0.526), nc22 142.0k, nc33 132.3k, s2 156.5k -> the default build keeps NC = 0.
