@@ -593,6 +593,34 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
 // LDS tickets. Early stop is batch-global: pass 1 runs imax-1 iterations and records each CN pass's
 // syndrome in the per-pass path's flag words; finalize_iters turns them into L; pass 2 (dL set)
 // re-runs the batch to L only if L < imax-1.
+// The fused kernel's light node bodies (checks of degree <= 6, variables <= 4) run every group of the
+// dword's 8 codewords unrolled (the per-pass kernels keep `unroll 1` for their register budget; the
+// heavier bodies would spill): 2-4x the independent lookup chains per wave,
+// which the phase-separated fused schedule needs to keep the LDS busy with 16 waves per CU.
+#ifndef IBL_FUSED_UNROLL
+#define IBL_FUSED_UNROLL 1
+#endif
+template <int D>
+__device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
+                                              const uint32_t (&cb)[4], uint32_t (&o)[D]) {
+  if constexpr (IBL_FUSED_UNROLL && D <= 6) {
+#pragma unroll
+    for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, o, k0);
+  } else {
+    cn_word<D>(lane4, in, fbase, cb, o);
+  }
+}
+template <int D>
+__device__ __forceinline__ void fused_vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw, uint32_t fbase,
+                                              const uint32_t (&cb)[4], uint32_t (&o)[D]) {
+  if constexpr (IBL_FUSED_UNROLL && D <= 4) {
+#pragma unroll
+    for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);
+  } else {
+    vn_word<D>(lane4, in, chw, fbase, cb, o);
+  }
+}
+
 template <int D>
 __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt, int lane, uint32_t lane4,
                                                const IbFusedArgs& a, bool do_par, uint32_t vmask, bool& unsat) {
@@ -629,7 +657,7 @@ __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt
     }
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};   // no column-fetched inputs (checked on the host: ncs == 0)
-    cn_word<D>(lane4, in, fbase, cb, o);
+    fused_cn_word<D>(lane4, in, fbase, cb, o);
   }
 #pragma unroll
   for (int j = 0; j < D; ++j) msg[first + j * cnt + lane] = o[j];
@@ -678,7 +706,7 @@ __device__ __forceinline__ void fused_vn_dword(uint32_t* msg, const VnTask<MAXD>
     o[0] = v.chw;     // degree 1 forwards the channel value (:131-136)
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};
-    vn_word<D>(lane4, in, v.chw, slot_off(a.vn_fslot[D]), cb, o);
+    fused_vn_word<D>(lane4, in, v.chw, slot_off(a.vn_fslot[D]), cb, o);
   }
 #pragma unroll
   for (int k = 0; k < D; ++k) msg[v.sl[k]] = o[k];
