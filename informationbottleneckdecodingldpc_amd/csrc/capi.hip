@@ -187,7 +187,7 @@ struct ibl_float {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
-  int32_t f_ncn = 0, f_nvn = 0, f_maxd = 0;
+  int32_t f_ncn = 0, f_nvn = 0, f_maxd = 0, f_slot16 = 0;
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -777,7 +777,11 @@ int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_tas
 int fused_setup(ibl_float* h) {
   const ibl_graph* g = h->g;
   const int64_t E = g->n_e;
-  const size_t lds = (size_t)(E + g->n_v) * 16 + 16;
+  size_t lds = (size_t)(E + g->n_v) * 16 + 16;
+  // variable-edge slot indices as u16 in LDS when they fit (E < 65536 and the space is there)
+  const size_t lds16 = (size_t)(E + g->n_v) * 16 + 16 + (size_t)E * 2;
+  const bool slot16 = E < 65536 && lds16 <= (size_t)kLdsBytes;
+  if (slot16) lds = lds16;
   int min_dc = 1 << 30;
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
   if (lds > (size_t)kLdsBytes || min_dc < 2 || E == 0) return IBL_OK;
@@ -798,6 +802,7 @@ int fused_setup(ibl_float* h) {
   h->f_nvn = (int32_t)(vn_task.size() / 4);
   h->f_maxd = maxd;
   h->f_lds = lds;
+  h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
   h->fused_ok = true;
   return IBL_OK;
@@ -991,10 +996,28 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
     fa.n_vn_tasks = h->f_nvn; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
     fa.ngroups = (B + cwl - 1) / cwl;
+    fa.slot16 = h->f_slot16;
+    const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
+    const size_t ntr = (size_t)2 * (2 * I + 4);
+    if (ftrace) {
+      HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));
+      HIPCHK(hipMemsetAsync(fa.trace, 0, sizeof(uint64_t) * ntr, s));
+    }
     const size_t esz = out_dtype == kF32 ? 4 : 8;
     fa.aligned = ((B % cwl) == 0 && ((uintptr_t)d_out % (cwl * esz)) == 0) ? 1 : 0;
     const int grid = std::min(fa.ngroups, h->f_grid);
     HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, h->f_maxd, grid, h->f_lds, s); }));
+    if (ftrace) {
+      std::vector<uint64_t> hv(ntr);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(hv.data(), fa.trace, sizeof(uint64_t) * ntr, hipMemcpyDeviceToHost));
+      (void)hipFree(fa.trace);
+      fa.trace = nullptr;
+      if (FILE* fp = fopen(ftrace, "wb")) {
+        fwrite(hv.data(), sizeof(uint64_t), ntr, fp);
+        fclose(fp);
+      }
+    }
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     if (early) {   // batch-global stop before imax-1: re-run the batch to L (the kernel exits if L = imax-1)
       fa.unsat = nullptr;

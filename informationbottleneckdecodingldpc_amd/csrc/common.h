@@ -179,6 +179,9 @@ struct FlFusedArgs {
   const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
   double llr_max;
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, ldb, B, imax, out_dtype, aligned, ngroups;
+  int32_t slot16;           // 1: vn_slot staged into LDS as 16-bit indices (after 4 counter words)
+  uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED, -DIBL_FUSED_TRACE=1 builds): block 0's clock at
+                            // every phase end of its first group, else nullptr
 };
 
 struct FlDecArgs {

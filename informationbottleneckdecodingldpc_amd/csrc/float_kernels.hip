@@ -43,15 +43,30 @@ template <> struct Vec<double> {
   __device__ static void set(T& v, int s, double x) { if (s == 0) v.x = x; else v.y = x; }
 };
 
-template <typename F> __device__ __forceinline__ F ocl_sign(F x) {
-  return x > F(0) ? F(1) : (x < F(0) ? F(-1) : (x != x ? F(0) : x));
-}
-// sign(t) * min(llr_max, sign(t) * t)  (kernels_min_and_BP.cl:69,120)
-template <typename F> __device__ __forceinline__ F clampllr(F t, F lm) {
-  const F s = ocl_sign(t);
-  const F a = s * t;
-  return s * ((a < lm) ? a : lm);
-}
+// sign(t) * min(llr_max, sign(t) * t)  (kernels_min_and_BP.cl:69,120) is the clamp of t to
+// [-llr_max, llr_max] for every non-NaN t, signed zeros included (sign(+-0) = +-0 gives +-0 back):
+// one v_med3_f32 in fp32 instead of the 3 compares, 3 selects, 2 products and a min of the literal
+// form. (Messages are never NaN: channel LLRs are finite and every operation keeps them finite.)
+__device__ __forceinline__ float clampllr(float t, float lm) { return __builtin_amdgcn_fmed3f(t, -lm, lm); }
+__device__ __forceinline__ double clampllr(double t, double lm) { return fmin(fmax(t, -lm), lm); }
+
+// sign-bit arithmetic of the min-sum check node
+template <typename F> struct Bits;
+template <> struct Bits<float> {
+  using U = uint32_t;
+  static constexpr U kSign = 0x80000000u;
+  __device__ static U of(float x) { return __float_as_uint(x); }
+  __device__ static float from(U u) { return __uint_as_float(u); }
+  __device__ static float med3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+};
+template <> struct Bits<double> {
+  using U = uint64_t;
+  static constexpr U kSign = 0x8000000000000000ull;
+  __device__ static U of(double x) { return (U)__double_as_longlong(x); }
+  __device__ static double from(U u) { return __longlong_as_double((long long)u); }
+  // median of (lo <= hi, c): max(lo, min(hi, c))
+  __device__ static double med3(double lo, double hi, double c) { return fmax(lo, fmin(hi, c)); }
+};
 
 __device__ __forceinline__ double boxplus(double a, double b, double lm) {
   const double boxp = log((1.0 + exp(a + b)) / (exp(a) + exp(b)));
@@ -117,29 +132,36 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put
   constexpr int N = Vec<F>::N;
   F o[N];
   if constexpr (KIND == 0) {
-    // min-sum (kernels_min_and_BP.cl:156-162): |out_w| = min over the others, sign = product
+    // min-sum (kernels_min_and_BP.cl:156-162): the fold t = sgn(m t) min(|t|, |m|) over the others of
+    // output w only selects values, so |out_w| = min over the others = mn1, or mn2 where |m_w| is the
+    // minimum (on a tie mn2 == mn1), and its sign is the XOR of the others' sign bits. A zero input
+    // (sign() = 0 kills the reference's fold) makes mn1 = 0, so every other output is +-0 as there; the
+    // zero's own output is the others' min. Running (mn1, mn2) with v_min / v_med3 on |m| (abs is an
+    // input modifier), signs XORed as bits: ~2.5 VALU per input and 4 per output.
+    using Bt = Bits<F>;
+    using U = typename Bt::U;
     F mn1[N], mn2[N];
-    int idx[N], nz[N];
-    bool neg[N];
+    U sg[N];
 #pragma unroll
     for (int s = 0; s < N; ++s) {
-      mn1[s] = F(INFINITY); mn2[s] = F(INFINITY); idx[s] = -1; nz[s] = 0; neg[s] = false;
+      const F a0 = fabs(m[0][s]), a1 = fabs(m[1][s]);
+      mn1[s] = fmin(a0, a1);
+      mn2[s] = fmax(a0, a1);
+      sg[s] = Bt::of(m[0][s]) ^ Bt::of(m[1][s]);
 #pragma unroll
-      for (int j = 0; j < D; ++j) {
-        const F x = m[j][s] < F(0) ? -m[j][s] : m[j][s];
-        if (x < mn1[s]) { mn2[s] = mn1[s]; mn1[s] = x; idx[s] = j; } else if (x < mn2[s]) { mn2[s] = x; }
-        neg[s] ^= (m[j][s] < F(0));
-        nz[s] += (m[j][s] == F(0));
+      for (int j = 2; j < D; ++j) {
+        const F x = fabs(m[j][s]);
+        mn2[s] = Bt::med3(mn1[s], mn2[s], x);
+        mn1[s] = fmin(mn1[s], x);
+        sg[s] ^= Bt::of(m[j][s]);
       }
     }
 #pragma unroll
     for (int w = 0; w < D; ++w) {
 #pragma unroll
       for (int s = 0; s < N; ++s) {
-        const F mag = (w == idx[s]) ? mn2[s] : mn1[s];
-        const bool zw = (m[w][s] == F(0));
-        const bool ng = neg[s] ^ (m[w][s] < F(0));
-        o[s] = (nz[s] - (zw ? 1 : 0)) > 0 ? F(0) : (ng ? -mag : mag);
+        const F mag = (fabs(m[w][s]) == mn1[s]) ? mn2[s] : mn1[s];
+        o[s] = Bt::from(Bt::of(mag) | ((sg[s] ^ Bt::of(m[w][s])) & Bt::kSign));
       }
       put(w, o);
     }
@@ -527,9 +549,17 @@ __device__ __forceinline__ void fused_cn_item(typename Vec<F>::T* msg, int first
   });
 }
 
+// Variable-edge slot indices: staged into LDS as 16-bit values when they fit beside the messages (one
+// LDS read instead of an L2 round trip per variable task and phase), else read from global memory.
+struct SlotIdx {
+  const uint16_t* s16;   // LDS copy, or nullptr
+  const int32_t* s32;    // global array
+  __device__ __forceinline__ int operator[](int i) const { return s16 ? (int)s16[i] : s32[i]; }
+};
+
 template <typename F, int D>
 __device__ __forceinline__ void fused_vn_item(typename Vec<F>::T* msg, const typename Vec<F>::T* chL,
-                                              const int32_t* vn_slot, int pos, int sfirst, int cnt, int lane, F lm) {
+                                              const SlotIdx& vn_slot, int pos, int sfirst, int cnt, int lane, F lm) {
   using V = Vec<F>;
   constexpr int N = V::N;
   int sl[D];
@@ -567,10 +597,21 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
   if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+  SlotIdx vs{nullptr, a.vn_slot};
+  if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
+    uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
+    for (int i = threadIdx.x; i < a.n_e; i += blockDim.x) s16[i] = (uint16_t)a.vn_slot[i];
+    vs.s16 = s16;
+  }
   __syncthreads();
   int ph = 0;
   const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
   // one phase: tasks dealt by ticket; the next phase's counter is reset while this one runs
+#ifndef IBL_FUSED_TRACE
+#define IBL_FUSED_TRACE 0
+#endif
+  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && threadIdx.x == 0) ? a.trace : nullptr;
+  if (IBL_FUSED_TRACE && tr) tr[0] = __builtin_readcyclecounter();
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
@@ -579,8 +620,14 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
       if (t >= ntasks) break;
       body(t);
     }
+    if constexpr (IBL_FUSED_TRACE) {
+      if (tr) tr[2 * ph + 1] = __builtin_readcyclecounter();   // thread 0's wave done
+    }
     __syncthreads();
     ++ph;
+    if constexpr (IBL_FUSED_TRACE) {
+      if (tr) tr[2 * ph] = __builtin_readcyclecounter();       // every wave done
+    }
   };
   for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
     const int cw0 = grp * N;
@@ -593,7 +640,7 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
         const int node = a.vn_node[pos + lane];
         const VT c = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
         chL[pos + lane] = c;
-        for (int k = 0; k < d; ++k) msg[a.vn_slot[sf + k * cnt + lane]] = c;
+        for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
       }
     });
     for (int j = 1; j <= L; ++j) {
@@ -617,8 +664,8 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
         const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
         if (lane < cnt) {
           switch (d) {
-            case 1: fused_vn_item<F, 1>(msg, chL, a.vn_slot, pos + lane, sf, cnt, lane, lm); break;
-#define X(D) case D: if constexpr (D <= MAXD) fused_vn_item<F, D>(msg, chL, a.vn_slot, pos + lane, sf, cnt, lane, lm); break;
+            case 1: fused_vn_item<F, 1>(msg, chL, vs, pos + lane, sf, cnt, lane, lm); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_vn_item<F, D>(msg, chL, vs, pos + lane, sf, cnt, lane, lm); break;
             FL_DEG_CASES(X)
 #undef X
             default: break;
@@ -640,7 +687,7 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
         }
         if (L > 0)
           for (int k = 0; k < d; ++k) {
-            const VT r = msg[a.vn_slot[sf + k * cnt + lane]];
+            const VT r = msg[vs[sf + k * cnt + lane]];
 #pragma unroll
             for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
           }
@@ -670,6 +717,7 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
         }
       }
     });
+    tr = nullptr;   // trace the first group only
   }
 }
 
