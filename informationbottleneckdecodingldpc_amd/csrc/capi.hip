@@ -988,8 +988,8 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   const int cwl = h->prec == kF32 ? 4 : 2;
   const int nchunks = (B + 64 * cwl - 1) / (64 * cwl);
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
-  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, s));
   if (h->fused_ok && h->path != IBL_PATH_PASSES) {
+    HIPCHK(launch_fl_stage_t(d_llr, llr_dtype, g->n_v, B, h->f_vn_node, h->chf, h->prec, s));
     FlFusedArgs fa{};
     fa.ch = h->chf; fa.cn_task = h->f_cn_task; fa.vn_task = h->f_vn_task; fa.vn_node = h->f_vn_node;
     fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
@@ -1026,6 +1026,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     }
     return IBL_OK;
   }
+  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, s));
   FlArgs send{};
   send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
   send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;

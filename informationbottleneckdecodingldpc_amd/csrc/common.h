@@ -169,7 +169,7 @@ struct FlArgs {
 // one degree, lane = node): edge k of lane i of a task at slot first + k*count + i, so the check
 // pass reads and writes contiguous 16-byte slots; the variable pass gathers through vn_slot.
 struct FlFusedArgs {
-  const void* ch;           // staged channel LLRs [N][ldb] (F)
+  const void* ch;           // staged channel LLRs [group][variable position] (Vec<F>::T, fl_stage_t)
   const int32_t* cn_task;   // per check task: {first slot, count, degree, 0}
   const int32_t* vn_task;   // per variable task: {first position, count, degree, first vn_slot index}
   const int32_t* vn_node;   // variable position -> node
@@ -248,6 +248,8 @@ hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int
 
 hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s);
 hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s);
+hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm, void* dst, int prec,
+                             hipStream_t s);
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);

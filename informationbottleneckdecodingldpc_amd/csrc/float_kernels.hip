@@ -476,6 +476,44 @@ __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int 
   }
 }
 
+// channel staging for the fused decoder: user LLRs [N][B] -> [group][variable position] 16-byte slots
+// (Vec<F>::N codewords of variable perm[pos]), zero padded past B
+// Tiled through LDS (64 positions x 32 groups): rows read along the codewords, slots written along the
+// positions, both coalesced; tile rows padded by one element.
+template <typename F>
+__global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm,
+                                                  typename Vec<F>::T* dst) {
+  using V = Vec<F>;
+  constexpr int N = V::N, P = 64, G = 32, RW = G * N + 1;
+  __shared__ F tile[P * RW];
+  const int ngroups = (B + N - 1) / N;
+  const int ptiles = (n + P - 1) / P, gtiles = (ngroups + G - 1) / G;
+  for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
+    const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * G * N; i += blockDim.x) {
+      const int r = i / (G * N), c = i - r * (G * N);
+      const int b = g0 * N + c;
+      F val = F(0);
+      if (p0 + r < n && b < B) {
+        const size_t k = (size_t)perm[p0 + r] * B + b;
+        val = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
+      }
+      tile[r * RW + c] = val;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * G; i += blockDim.x) {
+      const int g = i / P, p = i - g * P;
+      if (p0 + p < n && g0 + g < ngroups) {
+        typename V::T o;
+#pragma unroll
+        for (int s = 0; s < N; ++s) V::set(o, s, tile[p * RW + g * N + s]);
+        dst[(size_t)(g0 + g) * n + p0 + p] = o;
+      }
+    }
+  }
+}
+
 // send_channel_values_to_checknode_inbox (kernels_min_and_BP.cl:12-29): scatter staged rows
 template <typename F>
 __global__ void fl_send(FlArgs a) {
@@ -637,8 +675,8 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
       const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
       const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
       if (lane < cnt) {
-        const int node = a.vn_node[pos + lane];
-        const VT c = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
+        // channel staged as [group][variable position] (fl_stage_t): a task reads consecutive slots
+        const VT c = reinterpret_cast<const VT*>(a.ch)[(size_t)grp * a.n_v + pos + lane];
         chL[pos + lane] = c;
         for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
       }
@@ -727,6 +765,16 @@ hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst,
   const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
   if (prec == kF32) hipLaunchKernelGGL(fl_stage<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (float*)dst, ldb);
   else hipLaunchKernelGGL(fl_stage<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (double*)dst, ldb);
+  return hipGetLastError();
+}
+
+hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm, void* dst, int prec,
+                             hipStream_t s) {
+  const int cwl = prec == kF32 ? 4 : 2;
+  const size_t tiles = (size_t)((n + 63) / 64) * (size_t)((((B + cwl - 1) / cwl) + 31) / 32);
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>(tiles, 8192));
+  if (prec == kF32) hipLaunchKernelGGL(fl_stage_t<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (float4*)dst);
+  else hipLaunchKernelGGL(fl_stage_t<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (double2*)dst);
   return hipGetLastError();
 }
 

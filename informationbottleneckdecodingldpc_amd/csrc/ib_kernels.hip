@@ -912,28 +912,48 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
 
 // channel staging for the fused decoder: user [N][B] (u8 / i32) -> chT [group][position] dwords of 8
 // nibbles, positions in variable-task order (perm[pos] = node), so a task's lanes read consecutive dwords
-__global__ void ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT) {
+// Tiled through LDS (64 positions x 512 codewords): rows are read along the codewords (coalesced), the
+// dwords are written along the positions (coalesced); tile rows padded by one dword (conflict-free reads).
+__global__ __launch_bounds__(256) void ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm,
+                                                  uint32_t* chT) {
+  constexpr int P = 64, G = 64, RW = 2 * G + 1;   // RW: dwords per tile row (4 codewords each) + pad
+  __shared__ uint32_t tile[P * RW];
   const int ngroups = (B + 7) >> 3;
-  const size_t total = (size_t)ngroups * n;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int g = (int)(i / n);
-    const int v = perm[(int)(i - (size_t)g * n)];
-    uint32_t packed = 0;
+  const int ptiles = (n + P - 1) / P, gtiles = (ngroups + G - 1) / G;
+  for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
+    const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * 2 * G; i += blockDim.x) {
+      const int r = i / (2 * G), c = i - r * (2 * G);
+      uint32_t w = 0;
+      if (p0 + r < n) {
+        const size_t row = (size_t)perm[p0 + r] * B;
+        const int cw = g0 * 8 + 4 * c;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int cw = g * 8 + s;
-      uint32_t x = 0;
-      if (cw < B) {
-        if (dtype == kU8) {
-          x = reinterpret_cast<const uint8_t*>(ch)[(size_t)v * B + cw];
-        } else {
-          const int32_t y = reinterpret_cast<const int32_t*>(ch)[(size_t)v * B + cw];
-          x = (uint32_t)min(max(y, 0), 255);
+        for (int s = 0; s < 4; ++s) {
+          if (cw + s < B) {
+            uint32_t x;
+            if (dtype == kU8) {
+              x = reinterpret_cast<const uint8_t*>(ch)[row + cw + s];
+            } else {
+              const int32_t y = reinterpret_cast<const int32_t*>(ch)[row + cw + s];
+              x = (uint32_t)min(max(y, 0), 255);
+            }
+            w |= min(x, 15u) << (8 * s);
+          }
         }
       }
-      packed |= min(x, 15u) << (4 * s);
+      tile[r * RW + c] = w;
     }
-    chT[i] = packed;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * G; i += blockDim.x) {
+      const int g = i / P, p = i - g * P;
+      if (p0 + p < n && g0 + g < ngroups) {
+        const uint32_t lo = tile[p * RW + 2 * g], hi = tile[p * RW + 2 * g + 1];
+        auto nib4 = [](uint32_t x) { return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u); };
+        chT[(size_t)(g0 + g) * n + p0 + p] = nib4(lo) | (nib4(hi) << 16);
+      }
+    }
   }
 }
 
@@ -1200,8 +1220,8 @@ hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const 
 }
 hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT,
                              hipStream_t s) {
-  const size_t total = (size_t)((B + 7) >> 3) * n;
-  const int grid = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, 16384));
+  const size_t tiles = (size_t)((n + 63) / 64) * (size_t)((((B + 7) >> 3) + 63) / 64);
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>(tiles, 8192));
   hipLaunchKernelGGL(ib_stage_t, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, perm, chT);
   return hipGetLastError();
 }
