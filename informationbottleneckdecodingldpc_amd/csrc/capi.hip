@@ -844,7 +844,39 @@ int build_fused_tasks(const ibl_graph* g, FusedTasks* ft) {
     }
   }
   {
-    const std::vector<int32_t> ord = sorted(g->h_vn_deg);
+    std::vector<int32_t> ord = sorted(g->h_vn_deg);
+    // Variable order within each degree: the variable pass reads its edge slots in check-task order,
+    // so lanes of one 32-lane group (one LDS cycle of a ds_read_b32) collide when their k-th slots share
+    // a bank (slot mod 32). Greedily fill each 32-lane group with variables whose k-th slots hit banks
+    // not yet used by the group at that k (scan window 256): the fused IB kernel's dword slots then read
+    // (almost) conflict-free. Any order gives the same results.
+    for (size_t i0 = 0; i0 < ord.size();) {
+      const int32_t d = g->h_vn_deg[ord[i0]];
+      size_t i1 = i0;
+      while (i1 < ord.size() && g->h_vn_deg[ord[i1]] == d) ++i1;
+      std::vector<int32_t> pool(ord.begin() + (long)i0, ord.begin() + (long)i1), res;
+      res.reserve(pool.size());
+      auto bank = [&](int32_t v, int k) { return (uint32_t)slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]] & 31u; };
+      while (!pool.empty()) {
+        uint32_t used[kMaxD + 1] = {0};
+        for (int lane = 0; lane < 32 && !pool.empty(); ++lane) {
+          size_t best = 0;
+          int bestc = 1 << 30;
+          const size_t win = std::min<size_t>(pool.size(), 256);
+          for (size_t c = 0; c < win && bestc > 0; ++c) {
+            int col = 0;
+            for (int k = 0; k < d && k <= kMaxD; ++k) col += (used[k] >> bank(pool[c], k)) & 1u;
+            if (col < bestc) { bestc = col; best = c; }
+          }
+          const int32_t v = pool[best];
+          for (int k = 0; k < d && k <= kMaxD; ++k) used[k] |= 1u << bank(v, k);
+          res.push_back(v);
+          pool.erase(pool.begin() + (long)best);
+        }
+      }
+      std::copy(res.begin(), res.end(), ord.begin() + (long)i0);
+      i0 = i1;
+    }
     int32_t sidx = 0;
     for (size_t i = 0; i < ord.size();) {
       const int32_t d = g->h_vn_deg[ord[i]];

@@ -491,15 +491,25 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
   for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
     const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
     __syncthreads();
-    for (int i = threadIdx.x; i < P * G * N; i += blockDim.x) {
+    // all of a thread's loads issued before its LDS stores (256 threads: P*G*N/256 elements each)
+    constexpr int kPer = P * G * N / 256;
+    F val[kPer];
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int i = threadIdx.x + it * 256;
       const int r = i / (G * N), c = i - r * (G * N);
       const int b = g0 * N + c;
-      F val = F(0);
+      val[it] = F(0);
       if (p0 + r < n && b < B) {
         const size_t k = (size_t)perm[p0 + r] * B + b;
-        val = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
+        val[it] = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
       }
-      tile[r * RW + c] = val;
+    }
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int r = i / (G * N), c = i - r * (G * N);
+      tile[r * RW + c] = val[it];
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P * G; i += blockDim.x) {

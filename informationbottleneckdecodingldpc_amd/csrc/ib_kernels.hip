@@ -923,27 +923,48 @@ __global__ __launch_bounds__(256) void ib_stage_t(const void* ch, int dtype, int
   for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
     const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
     __syncthreads();
-    for (int i = threadIdx.x; i < P * 2 * G; i += blockDim.x) {
+    // all of a thread's loads issued before its LDS stores (256 threads: 32 dwords of 4 codewords each);
+    // u8 rows whose 4-codeword words are aligned (B % 4 == 0) load one dword per word
+    constexpr int kPer = P * 2 * G / 256;
+    uint32_t w[kPer];
+    const bool words = dtype == kU8 && (B & 3) == 0;
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int i = threadIdx.x + it * 256;
       const int r = i / (2 * G), c = i - r * (2 * G);
-      uint32_t w = 0;
+      w[it] = 0;
       if (p0 + r < n) {
         const size_t row = (size_t)perm[p0 + r] * B;
         const int cw = g0 * 8 + 4 * c;
+        if (words) {
+          if (cw < B) w[it] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(ch) + row + cw);
+        } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          if (cw + s < B) {
-            uint32_t x;
-            if (dtype == kU8) {
-              x = reinterpret_cast<const uint8_t*>(ch)[row + cw + s];
-            } else {
-              const int32_t y = reinterpret_cast<const int32_t*>(ch)[row + cw + s];
-              x = (uint32_t)min(max(y, 0), 255);
+          for (int s = 0; s < 4; ++s) {
+            if (cw + s < B) {
+              uint32_t x;
+              if (dtype == kU8) {
+                x = reinterpret_cast<const uint8_t*>(ch)[row + cw + s];
+              } else {
+                const int32_t y = reinterpret_cast<const int32_t*>(ch)[row + cw + s];
+                x = (uint32_t)min(max(y, 0), 255);
+              }
+              w[it] |= x << (8 * s);
             }
-            w |= min(x, 15u) << (8 * s);
           }
         }
       }
-      tile[r * RW + c] = w;
+    }
+#pragma unroll
+    for (int it = 0; it < kPer; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int r = i / (2 * G), c = i - r * (2 * G);
+      // bytes clamped to 15 (cluster ids of the fast path's 16-level alphabet)
+      const uint32_t x = w[it];
+      uint32_t y = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) y |= min((x >> (8 * s)) & 0xFFu, 15u) << (8 * s);
+      tile[r * RW + c] = y;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P * G; i += blockDim.x) {
