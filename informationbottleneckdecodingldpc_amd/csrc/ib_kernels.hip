@@ -111,21 +111,55 @@ template <> struct RowVec<1> { typedef uint32_t T; };
 template <> struct RowVec<2> { typedef uint2 T; };
 template <> struct RowVec<4> { typedef uint4 T; };
 
-template <int W>
+// IBL_NT: message rows are streamed once per pass (0.93 GB per inbox at B = 8192, far beyond the
+// caches): 1 = nontemporal loads and stores of the variable pass's rows (the HBM-bound pass; variant
+// nt, tools/variants.py). The check pass keeps plain accesses (its registers are at the cap).
+#ifndef IBL_NT
+#define IBL_NT 0
+#endif
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+template <int W> struct RowNV;
+template <> struct RowNV<1> { typedef uint32_t T; };
+template <> struct RowNV<2> { typedef u32x2_t T; };
+template <> struct RowNV<4> { typedef u32x4_t T; };
+
+template <int W, bool NT = false>
 __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&r)[W]) {
-  const auto v = *reinterpret_cast<const typename RowVec<W>::T*>(p);
-  if constexpr (W == 1) {
-    r[0] = v;
-  } else if constexpr (W == 2) {
-    r[0] = v.x; r[1] = v.y;
+  if constexpr (NT) {
+    using T = typename RowNV<W>::T;
+    const T v = __builtin_nontemporal_load(reinterpret_cast<const T*>(p));
+    if constexpr (W == 1) {
+      r[0] = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < W; ++i) r[i] = v[i];
+    }
   } else {
-    r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    const auto v = *reinterpret_cast<const typename RowVec<W>::T*>(p);
+    if constexpr (W == 1) {
+      r[0] = v;
+    } else if constexpr (W == 2) {
+      r[0] = v.x; r[1] = v.y;
+    } else {
+      r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+    }
   }
 }
 
-template <int W>
+template <int W, bool NT = false>
 __device__ __forceinline__ void store_row(uint8_t* p, const uint32_t (&r)[W]) {
-  if constexpr (W == 1) {
+  if constexpr (NT) {
+    using T = typename RowNV<W>::T;
+    T v;
+    if constexpr (W == 1) {
+      v = r[0];
+    } else {
+#pragma unroll
+      for (int i = 0; i < W; ++i) v[i] = r[i];
+    }
+    __builtin_nontemporal_store(v, reinterpret_cast<T*>(p));
+  } else if constexpr (W == 1) {
     *reinterpret_cast<uint32_t*>(p) = r[0];
   } else if constexpr (W == 2) {
     *reinterpret_cast<uint2*>(p) = make_uint2(r[0], r[1]);
@@ -173,10 +207,10 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    load_row<W>(row + b.off, b.row[j]);
+    load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
   }
   if (VN) {
-    load_row<W>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
+    load_row<W, IBL_NT>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
   } else {
 #pragma unroll
     for (int i = 0; i < W; ++i) b.chw[i] = 0;
@@ -336,7 +370,7 @@ __device__ __forceinline__ void vn_compute(const IbFastArgs& a, uint32_t lane4, 
     }
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+  for (int w = 0; w < D; ++w) store_row<W, IBL_NT>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ------------------------------------------------------------- decision output
