@@ -112,10 +112,11 @@ template <> struct RowVec<2> { typedef uint2 T; };
 template <> struct RowVec<4> { typedef uint4 T; };
 
 // IBL_NT: message rows are streamed once per pass (0.93 GB per inbox at B = 8192, far beyond the
-// caches): 1 = nontemporal loads and stores of the variable pass's rows (the HBM-bound pass; variant
-// nt, tools/variants.py). The check pass keeps plain accesses (its registers are at the cap).
+// caches): 1 = nontemporal loads and stores of the variable pass's rows (the HBM-bound pass). The
+// check pass keeps plain accesses (its registers are at the cap). A/B on one box (tools/ab.sh, DVB-S2
+// B=8192, 2 reps): plain 163.3k cw/s (CN 0.4936 / VN 0.4936 ms), nontemporal 165.3k (0.4888 / 0.4860).
 #ifndef IBL_NT
-#define IBL_NT 0
+#define IBL_NT 1
 #endif
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));

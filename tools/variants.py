@@ -24,8 +24,8 @@ VARIANTS = {
     "mix1": ["IBL_MIX=1"],
     "mix2": ["IBL_MIX=2"],
     "mix3": ["IBL_MIX=3"],
-    # nontemporal message-row loads / stores in the per-pass IB kernels
-    "nt": ["IBL_NT=1"],
+    # plain (cached) variable-pass row accesses instead of the default nontemporal ones
+    "nt0": ["IBL_NT=0"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
