@@ -447,7 +447,13 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 // current one. Degrees dispatch to fully unrolled bodies (wave-uniform switch). Positions are
 // heaviest-first: [0, n_heavy) run with a MAXD-row item buffer, the rest with a kLightD-row one
 // (a degree-2 node then issues 4 row loads, not MAXD).
-template <class Buf, bool VN, bool GATHER, int DLO>
+// DEPTH: items in flight per wave (2 = ping-pong; 3 for the variable pass's light phase, whose items
+// are HBM-bound: A/B on one box, DVB-S2 B=8192, 2 reps: depth 2 VN 0.4618 ms / 174.1k cw/s, depth 3
+// 0.4570 ms / 174.7k)
+#ifndef IBL_LIGHT_DEPTH
+#define IBL_LIGHT_DEPTH 3
+#endif
+template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
                                          int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat,
                                          uint64_t* trace_items) {
@@ -482,27 +488,58 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
   // and the compiler's wait for the current item leaves the next item's loads in flight.
   const int base = first + (int)blockIdx.x * wpb;
   auto item_of = [&](int k) { return base + (k % wpb) + nw * (k / wpb); };
-  Buf A, Bb;
-  int item = item_of(take_ticket(ctr, lane));
-  if (item >= end) return;
   int done = 0;
-  fetch_item<Buf, VN, GATHER>(a, item, lane, A);
-  int kn = take_ticket(ctr, lane);
-  for (;;) {
-    int next = item_of(kn);
-    fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb);
-    kn = take_ticket(ctr, lane);
-    compute(A);
-    ++done;
-    if (next >= end) break;
-    item = next;
-    next = item_of(kn);
-    fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A);
-    kn = take_ticket(ctr, lane);
-    compute(Bb);
-    ++done;
-    if (next >= end) break;
-    item = next;
+  if constexpr (DEPTH == 3) {
+    // three buffers in rotation (light phase, HBM-bound): item k+2 is fetched before item k is computed
+    Buf A, Bb, Cc;
+    int ia = item_of(take_ticket(ctr, lane));
+    if (ia >= end) return;
+    fetch_item<Buf, VN, GATHER>(a, ia, lane, A);
+    int ib = item_of(take_ticket(ctr, lane));
+    fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb);
+    int kn = take_ticket(ctr, lane);
+    for (;;) {
+      int ic = item_of(kn);
+      fetch_item<Buf, VN, GATHER>(a, min(ic, end - 1), lane, Cc);
+      kn = take_ticket(ctr, lane);
+      compute(A);
+      ++done;
+      if (ib >= end) break;
+      ia = item_of(kn);
+      fetch_item<Buf, VN, GATHER>(a, min(ia, end - 1), lane, A);
+      kn = take_ticket(ctr, lane);
+      compute(Bb);
+      ++done;
+      if (ic >= end) break;
+      ib = item_of(kn);
+      fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb);
+      kn = take_ticket(ctr, lane);
+      compute(Cc);
+      ++done;
+      if (ia >= end) break;
+    }
+  } else {
+    Buf A, Bb;
+    int item = item_of(take_ticket(ctr, lane));
+    if (item >= end) return;
+    fetch_item<Buf, VN, GATHER>(a, item, lane, A);
+    int kn = take_ticket(ctr, lane);
+    for (;;) {
+      int next = item_of(kn);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb);
+      kn = take_ticket(ctr, lane);
+      compute(A);
+      ++done;
+      if (next >= end) break;
+      item = next;
+      next = item_of(kn);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A);
+      kn = take_ticket(ctr, lane);
+      compute(Bb);
+      ++done;
+      if (next >= end) break;
+      item = next;
+    }
   }
   // trace word {items | cu << 32}: accumulated in memory, not in a register live across the passes
   if (trace_items && lane == 0) *trace_items += (uint64_t)done;
@@ -540,7 +577,7 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
       ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
                                                       trace_items);
     else
-      ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
+      ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2)>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
                                                    unsat, trace_items);
   }
   if (a.trace && lane == 0) {

@@ -24,6 +24,8 @@ VARIANTS = {
     "mix1": ["IBL_MIX=1"],
     "mix2": ["IBL_MIX=2"],
     "mix3": ["IBL_MIX=3"],
+    # two light variable items in flight per wave (ping-pong) instead of three
+    "ld2": ["IBL_LIGHT_DEPTH=2"],
     # plain (cached) variable-pass row accesses instead of the default nontemporal ones
     "nt0": ["IBL_NT=0"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
