@@ -1030,7 +1030,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.ngroups = (B + cwl - 1) / cwl;
     fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
-    const size_t ntr = (size_t)2 * (2 * I + 4);
+    const size_t ntr = (size_t)34 * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));
       HIPCHK(hipMemsetAsync(fa.trace, 0, sizeof(uint64_t) * ntr, s));

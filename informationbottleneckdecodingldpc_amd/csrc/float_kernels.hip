@@ -658,23 +658,31 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(Fl
 #ifndef IBL_FUSED_TRACE
 #define IBL_FUSED_TRACE 0
 #endif
-  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && threadIdx.x == 0) ? a.trace : nullptr;
-  if (IBL_FUSED_TRACE && tr) tr[0] = __builtin_readcyclecounter();
+  // phase trace of block 0's first group (diagnostic builds): per phase 34 words — [0] start, [1 + w]
+  // wave w's done clock, [17 + w] its task count
+  const int wv = threadIdx.x >> 6;
+  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && lane == 0) ? a.trace : nullptr;
+  if (IBL_FUSED_TRACE && tr && wv == 0) tr[0] = __builtin_readcyclecounter();
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    int taken = 0;
     for (;;) {
       const int t = take_ticket(c, lane);
       if (t >= ntasks) break;
       body(t);
+      ++taken;
     }
     if constexpr (IBL_FUSED_TRACE) {
-      if (tr) tr[2 * ph + 1] = __builtin_readcyclecounter();   // thread 0's wave done
+      if (tr) {
+        tr[34 * ph + 1 + wv] = __builtin_readcyclecounter();
+        tr[34 * ph + 17 + wv] = (uint64_t)taken;
+      }
     }
     __syncthreads();
     ++ph;
     if constexpr (IBL_FUSED_TRACE) {
-      if (tr) tr[2 * ph] = __builtin_readcyclecounter();       // every wave done
+      if (tr && wv == 0) tr[34 * ph] = __builtin_readcyclecounter();
     }
   };
   for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {

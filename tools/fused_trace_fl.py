@@ -1,13 +1,19 @@
-"""Phase timeline of the fused float kernel (IBL_TRACE_FUSED dump, block 0's first group):
-python tools/fused_trace_fl.py <file>: per phase, thread 0's wave done and all waves done (cycles)."""
+"""Phase timeline of the fused float kernel (IBL_TRACE_FUSED dump, block 0's first group, diagnostic
+build `tools/variants.py ftrace`): python tools/fused_trace_fl.py <file> [phase ...]
+Per phase: duration to the barrier, and per wave (done clock - phase start, tasks taken)."""
 import sys
 
 import numpy as np
 
-t = np.fromfile(sys.argv[1], dtype=np.uint64).astype(np.int64)
-t0 = t[0]
+t = np.fromfile(sys.argv[1], dtype=np.uint64).astype(np.int64).reshape(-1, 34)
+show = [int(x) for x in sys.argv[2:]]
 ph = 0
-while 2 * ph + 2 < len(t) and t[2 * ph + 2] > 0:
-    start = t[2 * ph]
-    print(f"phase {ph:3d}: start {start - t0:9d} wave0 {t[2 * ph + 1] - start:7d} all {t[2 * ph + 2] - start:7d}")
+while ph + 1 < len(t) and t[ph + 1, 0] > 0:
+    start, end = t[ph, 0], t[ph + 1, 0]
+    done = t[ph, 1:17] - start
+    tasks = t[ph, 17:33]
+    line = f"phase {ph:3d}: {end - start:7d} cycles; waves done min/med/max {done.min()}/{int(np.median(done))}/{done.max()}"
+    if ph in show:
+        line += "\n   " + " ".join(f"{d}:{k}" for d, k in zip(done, tasks))
+    print(line)
     ph += 1
