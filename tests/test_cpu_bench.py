@@ -1,0 +1,68 @@
+"""CPU: bench.py's measurement arithmetic (no GPU): SURVEY §8(d) bytes per codeword and the roofline
+objects — priced at the bytes each kernel moves, so frac = achieved / peak <= 1 for physical timings."""
+import types
+
+import numpy as np
+import pytest
+
+import bench
+from informationbottleneckdecodingldpc_amd import codes, graph
+
+
+def _args(**kw):
+    a = types.SimpleNamespace(kind="ib", pmc="/nonexistent", config=None)
+    a.__dict__.update(kw)
+    return a
+
+
+def test_bytes_per_codeword_dvbs2():
+    # i_max (4E + N) + 2N with u8 messages: 48.73 MB at i_max = 50
+    assert bench.bytes_per_cw(226799, 64800, 50, 1) == 50 * (4 * 226799 + 64800) + 2 * 64800
+    assert abs(bench.bytes_per_cw(226799, 64800, 50, 1) / 1e6 - 48.73) < 0.01
+
+
+@pytest.fixture(scope="module")
+def dvb():
+    return graph.build_graph(codes.dvbs2_structured(seed=0))
+
+
+def test_ib_fast_roofline_prices_u4_bytes(dvb):
+    g, B = dvb, 8192
+    r = bench.roofline(_args(), g, g.n_v, B, 50, 1, 0.5, "u4", True, False,
+                       cn_avg=0.464, vn_avg=0.458, cn_ms=0.464 * 50, vn_ms=0.458 * 49, cn_n=50, vn_n=49, dec=None)
+    assert r["bound"] == "hbm" and r["format"] == "u4"
+    # the CN pass (50 launches) dominates: E*B/2 read + E*B/2 written
+    assert r["kernel"] == "ib_cn_fast" and r["bytes_per_launch"] == g.n_e * B
+    assert r["frac"] == pytest.approx(g.n_e * B / 0.464e-3 / 1e9 / bench.HBM_PEAK_GBPS, rel=1e-3)
+    assert 0 < r["frac"] <= 1
+    assert r["u8_equivalent"]["bytes_per_launch"] == 2 * g.n_e * B
+    lk = r["lds_lookups_per_clk_per_cu"]
+    assert lk["ceiling"] == 32.0 and 0 < lk["cn"] < 32 and 0 < lk["vn"] < 32
+
+
+def test_fused_rooflines_are_lds_bound():
+    g = graph.build_graph(codes.regular_code(8000, 3, 6, seed=0))
+    r = bench.roofline(_args(), g, g.n_v, 65536, 50, 1, 0.5, "u4", False, True,
+                       cn_avg=37.5, vn_avg=0.0, cn_ms=37.5, vn_ms=0.0, cn_n=1, vn_n=0, dec=None)
+    assert r["bound"] == "lds" and r["kernel"] == "ib_fused" and 0 < r["frac"] <= 1
+    w = graph.build_graph(codes.wlan_80211n(81))
+    f = bench.roofline(_args(kind="minsum"), w, w.n_v, 262144, 50, 4, 4, "f32", False, True,
+                       cn_avg=55.3, vn_avg=0.0, cn_ms=55.3, vn_ms=0.0, cn_n=1, vn_n=0, dec=None)
+    assert f["bound"] == "lds" and f["kernel"] == "fl_fused" and 0 < f["frac"] <= 1
+    # LDS peak at the 16-byte slot mix lies between the write (79 B/clk) and read (256 B/clk) rates
+    per_clk = f["peak"] / (bench.NUM_CUS * bench.LDS_CLK_GHZ)
+    assert 79 <= per_clk <= 256
+
+
+def test_numpy_host_baseline_workers(tmp_path):
+    """The spawned numpy decode_on_host workers reproduce the in-process decoder."""
+    from informationbottleneckdecodingldpc_amd import tables
+    from oracle.host_numpy import HostDecoder
+    g = graph.build_graph(codes.regular_code(504, 3, 6, seed=7))
+    tb = tables.random_tables(16, 16, 6, 3, 4, seed=2)
+    x = np.random.default_rng(0).integers(0, 16, (g.n_v, 6)).astype(np.int32)
+    outs, per_core, agg, wall = bench.numpy_host_baseline(g, tb, x, 4, True, 2)
+    ref = HostDecoder(g, 16, 16, 4, tb.cn, tb.vn, regular=True)
+    for k in range(6):
+        np.testing.assert_array_equal(outs[:, k], ref.decode(x[:, k]))
+    assert per_core > 0 and agg > 0 and wall > 0
