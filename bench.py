@@ -8,7 +8,7 @@ Default = BASELINE config C4 (the headline metric). The other presets measure th
 configs of BASELINE.json: C1 regular (3,6) N=8000 IB T=16 i_max=10, 1000 codewords (the reference's
 CPU case: its numpy decode_on_host, restated in oracle/host_numpy.py, is the cpu_baseline, one
 process per host core, next to the GPU decoding the same 1000 codewords); C2 regular (3,6) N=8000
-IB T=16 i_max=50, 65536 codewords; C3 WLAN N=1944 (802.11n-structured, Z=81) min-sum fp32
+IB T=16 i_max=50, 65536 codewords; C3 WLAN 802.11n N=1944 (the standard's Z=81 table) min-sum fp32
 i_max=50, 262144 codewords; C5 DVB-S2 BP fp32 i_max=100, 8192 codewords per GPU. The regular
 configs run without matching (the reference's regular class has none).
 
@@ -73,7 +73,7 @@ def parse():
 
 CODES = {"dvbs2": ("DVB-S2 N=64800 R=1/2", "DVB-S2-structured R=1/2 code (EN 302 307 profile, synthetic addresses)"),
          "regular": ("regular (3,6) N=8000", "seeded (3,6)-regular N=8000 code (stands in for MacKay 8000.4000.3.483)"),
-         "wlan": ("WLAN 802.11n N=1944 R=1/2", "802.11n R=1/2 base matrix lifted with Z=81 (WLAN-structured)")}
+         "wlan": ("WLAN 802.11n N=1944 R=1/2", "802.11n R=1/2 Z=81 prototype (IEEE 802.11-2012 Table F.2)")}
 
 
 def make_code(name):

@@ -16,8 +16,8 @@ Generators (the reference ships no matrices):
 
 * :func:`wlan_80211n` re-implements the quasi-cyclic expansion of
   ``Irregular_LDPC_Decoding/WLAN/generate_802.11_matrix.py:7-34`` (Z=54, N=1296);
-  ``Z=81`` gives a *WLAN-structured* N=1944 code (same base matrix, not the standard's
-  Z=81 shift table, which the reference does not contain).
+  ``Z=81`` uses the standard's own Z=81 rate-1/2 table (:data:`WLAN_R12_BASE_Z81`, N=1944 —
+  BASELINE config C3), which the reference does not contain.
 * :func:`regular_code` builds a seeded (d_v, d_c)-regular code without double edges,
   standing in for MacKay's ``8000.4000.3.483`` used by
   ``Regular_LDPC_Decoding/BPSK/BER_simulation_OpenCL.py:35``.
@@ -40,6 +40,7 @@ __all__ = [
     "save_sparse_csr",
     "wlan_80211n",
     "WLAN_R12_BASE",
+    "WLAN_R12_BASE_Z81",
     "regular_code",
     "dvbs2_structured",
     "code_rate",
@@ -126,15 +127,42 @@ WLAN_R12_BASE = np.array([
 ], dtype=np.int64)
 
 
-def wlan_80211n(Z: int = 54) -> sp.csr_matrix:
-    """Quasi-cyclic expansion of :data:`WLAN_R12_BASE` with lifting size ``Z``.
+# IEEE 802.11n (802.11-2012 Annex F, Table F.2) rate-1/2 prototype for Z=81 (N=1944), restated
+# from the standard: the reference holds only the Z=54 table above, so this table is not pinned by
+# a reference output. Structural checks (tests/test_cpu_host.py): the standard's dual-diagonal parity
+# part (column 12 shifts 1/0/1), the same column weights as the Z=54 table, and no 4-cycles after
+# lifting.
+WLAN_R12_BASE_Z81 = np.array([
+    [57, -1, -1, -1, 50, -1, 11, -1, 50, -1, 79, -1, 1, 0, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1],
+    [3, -1, 28, -1, 0, -1, -1, -1, 55, 7, -1, -1, -1, 0, 0, -1, -1, -1, -1, -1, -1, -1, -1, -1],
+    [30, -1, -1, -1, 24, 37, -1, -1, 56, 14, -1, -1, -1, -1, 0, 0, -1, -1, -1, -1, -1, -1, -1, -1],
+    [62, 53, -1, -1, 53, -1, -1, 3, 35, -1, -1, -1, -1, -1, -1, 0, 0, -1, -1, -1, -1, -1, -1, -1],
+    [40, -1, -1, 20, 66, -1, -1, 22, 28, -1, -1, -1, -1, -1, -1, -1, 0, 0, -1, -1, -1, -1, -1, -1],
+    [0, -1, -1, -1, 8, -1, 42, -1, 50, -1, -1, 8, -1, -1, -1, -1, -1, 0, 0, -1, -1, -1, -1, -1],
+    [69, 79, 79, -1, -1, -1, 56, -1, 52, -1, -1, -1, 0, -1, -1, -1, -1, -1, 0, 0, -1, -1, -1, -1],
+    [65, -1, -1, -1, 38, 57, -1, -1, 72, -1, 27, -1, -1, -1, -1, -1, -1, -1, -1, 0, 0, -1, -1, -1],
+    [64, -1, -1, -1, 14, 52, -1, -1, 30, -1, -1, 32, -1, -1, -1, -1, -1, -1, -1, -1, 0, 0, -1, -1],
+    [-1, 45, -1, 70, 0, -1, -1, -1, 77, 9, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0, 0, -1],
+    [2, 56, -1, 57, 35, -1, -1, -1, -1, -1, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0, 0],
+    [24, -1, 61, -1, 60, -1, -1, 27, 51, -1, -1, 16, 1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, 0],
+], dtype=np.int64)
+
+
+def wlan_80211n(Z: int = 54, base=None) -> sp.csr_matrix:
+    """Quasi-cyclic expansion of an 802.11n rate-1/2 prototype with lifting size ``Z``.
+
+    ``base`` defaults to the standard's table for ``Z``: :data:`WLAN_R12_BASE_Z81` for Z=81
+    (N=1944), else :data:`WLAN_R12_BASE` (the reference's Z=54 table; other Z give
+    WLAN-structured codes). Pass ``base=WLAN_R12_BASE`` to lift the Z=54 table at Z=81.
 
     Block (i, j) with shift s is the Z×Z identity rolled right by s columns, i.e. row r
     of the block has its 1 in column (r + s) mod Z — the same matrix
     ``np.roll(np.eye(Z), s, axis=1)`` builds in ``generate_802.11_matrix.py:28``.
     Z=54 reproduces the reference's 648×1296 matrix (E=4644).
     """
-    base = WLAN_R12_BASE
+    if base is None:
+        base = WLAN_R12_BASE_Z81 if Z == 81 else WLAN_R12_BASE
+    base = np.asarray(base, dtype=np.int64)
     mb, nb = base.shape
     rows, cols = [], []
     r = np.arange(Z)

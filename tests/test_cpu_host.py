@@ -98,8 +98,16 @@ def test_wlan_z81_structure():
     g = graph.build_graph(codes.wlan_80211n(81))
     assert (g.n_c, g.n_v) == (972, 1944)
     assert set(g.cn_deg) == {7, 8} and set(g.vn_deg) == {2, 3, 4, 11}
-
-
+    # the standard's Z=81 table (not held by the reference): same column weights as the Z=54
+    # table, the dual-diagonal parity part, and girth >= 6 after lifting (no 4-cycles)
+    b81, b54 = codes.WLAN_R12_BASE_Z81, codes.WLAN_R12_BASE
+    assert ((b81 >= 0).sum(0) == (b54 >= 0).sum(0)).all() and (b81 >= 0).sum() == 86
+    assert list(b81[[0, 6, 11], 12]) == [1, 0, 1] and (b81[:, 12][[1, 2, 3, 4, 5, 7, 8, 9, 10]] < 0).all()
+    H = codes.wlan_80211n(81).toarray()
+    assert (H[:, 1296:] != codes.wlan_80211n(81, base=b54).toarray()[:, 1296:]).sum() == 0  # same parity part
+    overlap = H @ H.T
+    np.fill_diagonal(overlap, 0)
+    assert overlap.max() <= 1  # two checks share at most one variable: no 4-cycles
 def test_table_lengths_follow_reference_layout():
     # Discrete_Density_Evolution.py:92-95 / :120-122 for the DVB-S2 profile (SURVEY §8 LUT lengths)
     assert tables.cn_lut_len(16, 16, 7, 50) == 256 + 4 * 256 + 49 * 5 * 256
