@@ -167,7 +167,7 @@ struct ibl_ib {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
-  int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0;
+  int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0;
   size_t f_lds = 0;
   int f_grid = 0, f_block = 0;
   // generic path
@@ -620,7 +620,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     f.out = d_out; f.unsat = early ? h->flags : nullptr; f.dL = nullptr;
     std::memcpy(f.cn_fslot, h->cn_fslot, sizeof(f.cn_fslot));
     std::memcpy(f.vn_fslot, h->vn_fslot, sizeof(f.vn_fslot));
-    f.cn_nt = h->cn_nt; f.vn_nt = h->vn_nt; f.dec_nt = h->dec_nt; f.nreg = h->f_nreg;
+    f.cn_nt = h->cn_nt; f.vn_nt = h->vn_nt; f.dec_nt = h->dec_nt; f.nreg = h->f_nreg; f.dbuf = h->f_dbuf;
     f.n_e = (int32_t)g->n_e; f.n_v = g->n_v; f.n_cn_tasks = h->f_ncn; f.n_vn_tasks = h->f_nvn;
     f.B = B; f.imax = I; f.half = h->T / 2; f.match = h->match; f.out_dtype = out_dtype;
     const size_t esz = out_dtype == kU8 ? 1 : 4;
@@ -906,8 +906,13 @@ int ib_fused_setup(ibl_ib* h) {
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
   if (min_dc < 2) return IBL_OK;
   const int nreg = std::max(h->cn_nt, std::max(h->vn_nt, h->dec_nt));
-  const size_t lds = (size_t)nreg * (kRegion + 1024) + (size_t)g->n_e * 4 + 16;   // tables, raw images, slots
+  size_t lds = (size_t)nreg * (kRegion + 1024) + (size_t)g->n_e * 4 + 16;   // tables, raw images, slots
   if (lds > (size_t)kLdsBytes) return IBL_OK;
+  // two table sets (see TablePrefetch) where they fit beside the slots; IBL_FUSED_DBUF=0 turns them off (A/B)
+  const size_t lds2 = (size_t)nreg * 2 * kRegion + (size_t)g->n_e * 4 + 16;
+  const char* dbe = getenv("IBL_FUSED_DBUF");
+  const bool dbuf = lds2 <= (size_t)kLdsBytes && !(dbe && dbe[0] == '0');
+  if (dbuf) lds = lds2;
   int bpc = 0, block = 0;
   size_t priv = 0;
   if (ib_fused_occupancy(h->CM, h->VM, lds, &bpc, &block, &priv) != hipSuccess || bpc < 1 || priv != 0) {
@@ -922,6 +927,7 @@ int ib_fused_setup(ibl_ib* h) {
   h->f_ncn = (int32_t)(ft.cn_task.size() / 4);
   h->f_nvn = (int32_t)(ft.vn_task.size() / 4);
   h->f_nreg = nreg;
+  h->f_dbuf = dbuf ? 1 : 0;
   h->f_lds = lds;
   h->f_block = block;
   h->f_grid = bpc * g->num_cus;

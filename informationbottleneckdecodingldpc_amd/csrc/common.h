@@ -115,6 +115,8 @@ struct IbFusedArgs {
   const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
   int32_t cn_fslot[kMaxD + 1], vn_fslot[kMaxD + 1];
   int32_t cn_nt, vn_nt, dec_nt, nreg;   // regions per pass image; nreg = table regions reserved in LDS
+  int32_t dbuf;             // 1: two table sets of nreg regions (phase p reads set p & 1; the next phase's
+                            // set is written during the current phase), no raw buffer
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, B, imax, half, match, out_dtype, aligned, ngroups;
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED): block 0's clock at every phase boundary of its
                             // first group, else nullptr

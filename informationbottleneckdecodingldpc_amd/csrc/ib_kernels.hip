@@ -807,25 +807,34 @@ __device__ __forceinline__ void fused_dec_dword(const uint32_t* msg, const VnTas
 }
 
 // Table staging: a pass's raw image is 256 dwords per region (each entry byte-packed 4 tables deep);
-// the LDS image replicates every dword over the 32 banks (l32[i] = img[i >> 5]). The next phase's raw
-// dwords are loaded into registers at the START of the current phase (2 per thread), written to a
-// small raw buffer in LDS when the wave's tasks are done, and replicated LDS -> LDS after the phase
-// barrier: the phase boundary pays LDS traffic only, not an L2 round trip.
+// the LDS image replicates every dword over the 32 banks (l32[i] = img[i >> 5]). Two modes:
+// * single set (dbuf = 0): the next phase's raw dwords are loaded into registers at the START of the
+//   current phase (2 per thread), written to a small raw buffer in LDS when the wave's tasks are done
+//   and replicated LDS -> LDS after the phase barrier (a second barrier follows): the phase boundary
+//   pays LDS traffic only, not an L2 round trip;
+// * two sets (dbuf = 1, when 2 x nreg regions fit beside the slots, e.g. regular (3,6) N=8000): phase p
+//   looks up in set p & 1. A thread loads one source dword per 8 replicated dwords of the next phase's
+//   image at the start of the current phase and writes them (two 16-byte stores of the same value) into
+//   the other set when its wave's tasks are done, i.e. while slower waves still compute: one barrier per
+//   phase and no serial replication step. The set is selected through the lookups' column term (lane4
+//   | set offset: the row/column part of an address stays below kRegion, so no extra VALU per lookup).
 constexpr int kPfSrc = 2;
 struct TablePrefetch {
   uint32_t r[kPfSrc];
   const uint32_t* img;
   int nsrc;   // raw dwords (nt * 256)
+  bool dbuf;
   __device__ __forceinline__ void load(const uint32_t* im, int nt) {
     img = im;
     nsrc = nt * 256;
+    const int n = dbuf ? nsrc * 4 : nsrc;   // dbuf: units of 8 replicated dwords
 #pragma unroll
     for (int k = 0; k < kPfSrc; ++k) {
       const int i = threadIdx.x + k * blockDim.x;
-      r[k] = i < nsrc ? img[i] : 0u;
+      r[k] = i < n ? img[dbuf ? (i >> 2) : i] : 0u;
     }
   }
-  // before the phase barrier: this thread's raw dwords into the raw buffer
+  // single set, before the phase barrier: this thread's raw dwords into the raw buffer
   __device__ __forceinline__ void put_raw(uint32_t* raw) const {
 #pragma unroll
     for (int k = 0; k < kPfSrc; ++k) {
@@ -834,11 +843,31 @@ struct TablePrefetch {
     }
     for (int i = threadIdx.x + kPfSrc * blockDim.x; i < nsrc; i += blockDim.x) raw[i] = img[i];
   }
-  // after the phase barrier: replicate into the table regions at LDS address 0
+  // single set, after the phase barrier: replicate into the table regions at LDS address 0
   __device__ __forceinline__ void replicate(uint8_t* lds, const uint32_t* raw) const {
     uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
     const int n = nsrc * 32;
     for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = raw[i >> 5];
+  }
+  // two sets, before the phase barrier: this thread's units straight into the next phase's set
+  __device__ __forceinline__ void put_set(uint8_t* set) const {
+    uint4* s4 = reinterpret_cast<uint4*>(set);
+    const int n = nsrc * 4;
+#pragma unroll
+    for (int k = 0; k < kPfSrc; ++k) {
+      const int i = threadIdx.x + k * blockDim.x;
+      if (i < n) {
+        const uint4 v = make_uint4(r[k], r[k], r[k], r[k]);
+        s4[2 * i] = v;
+        s4[2 * i + 1] = v;
+      }
+    }
+    for (int i = threadIdx.x + kPfSrc * blockDim.x; i < n; i += blockDim.x) {
+      const uint32_t w = img[i >> 2];
+      const uint4 v = make_uint4(w, w, w, w);
+      s4[2 * i] = v;
+      s4[2 * i + 1] = v;
+    }
   }
 };
 
@@ -852,12 +881,15 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   constexpr int MAXD = VMAX;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   lds_at_zero(lds);
-  // LDS: [nreg table regions][raw images, nreg x 1 KiB][E message slots][2 counters]
+  // LDS: [nreg table regions][raw images, nreg x 1 KiB][E message slots][2 counters], or with two
+  // table sets (dbuf): [set 0: nreg regions][set 1: nreg regions][E message slots][2 counters]
+  const uint32_t set_off = a.dbuf ? (uint32_t)a.nreg * kRegion : 0u;
   uint32_t* raw = reinterpret_cast<uint32_t*>(lds + (size_t)a.nreg * kRegion);
-  uint32_t* msg = raw + (size_t)a.nreg * 256;
+  uint32_t* msg = a.dbuf ? reinterpret_cast<uint32_t*>(lds + 2 * (size_t)set_off) : raw + (size_t)a.nreg * 256;
   int* ctr = reinterpret_cast<int*>(msg + a.n_e);
   const int lane = threadIdx.x & 63;
-  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const uint32_t lane4c = (uint32_t)(lane & 31) << 2;
+  uint32_t lane4 = lane4c;   // + the set offset of the current phase (dbuf)
   int L = a.imax - 1;
   if (a.dL) {
     L = __builtin_amdgcn_readfirstlane(*a.dL);
@@ -868,6 +900,7 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   int ph = 0;
   const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
   TablePrefetch pf;
+  pf.dbuf = a.dbuf != 0;
   // end of a phase: the next phase's raw tables into LDS, barrier (every wave done with the old
   // tables and slots), replication, barrier
   // phase trace (diagnostic builds only: -DIBL_FUSED_TRACE=1, tools/variants.py ftrace)
@@ -878,13 +911,21 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     }
   };
   auto next_phase = [&]() __attribute__((always_inline)) {
-    pf.put_raw(raw);
-    __syncthreads();
-    mark(3 * ph + 1);   // all waves done with the phase
-    pf.replicate(lds, raw);
-    __syncthreads();
-    mark(3 * ph + 2);   // next phase's tables staged
+    if (pf.dbuf) {
+      pf.put_set(lds + (((ph + 1) & 1) ? set_off : 0u));
+      __syncthreads();
+      mark(3 * ph + 1);   // all waves done with the phase (and the next phase's set written)
+      mark(3 * ph + 2);
+    } else {
+      pf.put_raw(raw);
+      __syncthreads();
+      mark(3 * ph + 1);   // all waves done with the phase
+      pf.replicate(lds, raw);
+      __syncthreads();
+      mark(3 * ph + 2);   // next phase's tables staged
+    }
     ++ph;
+    lane4 = lane4c | ((ph & 1) ? set_off : 0u);
     mark(3 * ph);       // next phase starts
   };
   // check tasks: slots are contiguous per task (no index loads)
@@ -978,6 +1019,7 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     __syncthreads();   // every wave done with this group's slots before the next group's send
     mark(3 * ph + 1);
     ++ph;
+    lane4 = lane4c | ((ph & 1) ? set_off : 0u);
     tr = nullptr;      // first group only
   }
 }

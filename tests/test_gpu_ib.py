@@ -152,6 +152,29 @@ def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn
     np.testing.assert_array_equal(po, ref)
 
 
+@pytest.mark.parametrize("name", ["reg8000", "wlan"])
+def test_ib_fused_table_sets(eng, name, wlan_H, monkeypatch):
+    """Both table-staging modes of the fused kernel (two LDS table sets where they fit, as for the
+    (3,6) N=8000 code; one set + raw buffer otherwise, forced with IBL_FUSED_DBUF=0) equal the oracle;
+    B = 4100 gives 513 groups of 8 codewords (a ragged last one), so workgroups run 2-3 groups and the
+    set parity carries across the group boundary."""
+    H = codes.regular_code(8000, 3, 6, seed=0) if name == "reg8000" else wlan_H
+    g = graph.build_graph(H)
+    G = eng.Graph(g, DEV)
+    q = UniformQuantizer(sigma2_from_ebn0(1.0, g.R_c), 16)
+    tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 11)
+    ch = q.sample_all_zero(g.n_v, 4100, np.random.default_rng(4)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=True, early_stop=False)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("IBL_FUSED_DBUF", mode)
+        fo, _, fdec = _run(eng, g, tb, ch, True, False, graph_obj=G, path="fused")
+        assert fdec.fused
+        outs.append(fo)
+    np.testing.assert_array_equal(outs[0], ref)
+    np.testing.assert_array_equal(outs[1], ref)
+
+
 def test_ib_fused_path_selection(eng, wlan_H, dvb_H):
     g = graph.build_graph(wlan_H)
     G = eng.Graph(g, DEV)
