@@ -167,7 +167,7 @@ struct ibl_ib {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
-  int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0;
+  int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
   int f_grid = 0, f_block = 0;
   // generic path
@@ -406,7 +406,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
   h->g = g;
   h->Tc = Tc; h->T = T; h->imax = imax; h->CM = CM; h->VM = VM; h->match = match ? 1 : 0;
   h->max_batch = max_batch;
-  h->ldb = (max_batch + kChunkIB - 1) / kChunkIB * kChunkIB;   // codewords; fast path rows = ldb/2 bytes
+  h->ldb = (max_batch + kRowPad - 1) / kRowPad * kRowPad;   // codewords; fast path rows = ldb/2 bytes
   auto bail = [&](int rc) { ibl_ib_destroy(h); return rc; };
   int rc;
   const size_t inbox = (size_t)g->n_e * h->ldb;
@@ -621,6 +621,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     std::memcpy(f.cn_fslot, h->cn_fslot, sizeof(f.cn_fslot));
     std::memcpy(f.vn_fslot, h->vn_fslot, sizeof(f.vn_fslot));
     f.cn_nt = h->cn_nt; f.vn_nt = h->vn_nt; f.dec_nt = h->dec_nt; f.nreg = h->f_nreg; f.dbuf = h->f_dbuf;
+    f.n_cn_nodes = g->n_c; f.cn_uni = h->f_cn_uni; f.vn_uni = h->f_vn_uni;
     f.n_e = (int32_t)g->n_e; f.n_v = g->n_v; f.n_cn_tasks = h->f_ncn; f.n_vn_tasks = h->f_nvn;
     f.B = B; f.imax = I; f.half = h->T / 2; f.match = h->match; f.out_dtype = out_dtype;
     const size_t esz = out_dtype == kU8 ? 1 : 4;
@@ -926,6 +927,23 @@ int ib_fused_setup(ibl_ib* h) {
     return rc;
   h->f_ncn = (int32_t)(ft.cn_task.size() / 4);
   h->f_nvn = (int32_t)(ft.vn_task.size() / 4);
+  // single-degree sides: task records follow from the task index (IbFusedArgs::cn_uni / vn_uni);
+  // IBL_FUSED_UNIFORM=0 keeps the loaded records (A/B)
+  const char* une = getenv("IBL_FUSED_UNIFORM");
+  if (!(une && une[0] == '0')) {
+    auto uniform = [](const std::vector<int32_t>& task, int32_t n, bool vn) {
+      if (task.empty()) return 0;
+      const int32_t d = task[2];
+      for (size_t t = 0; t < task.size() / 4; ++t) {
+        const int32_t p = (int32_t)(64 * t), cnt = std::min<int32_t>(64, n - p);
+        const int32_t* r = &task[4 * t];
+        if (r[1] != cnt || r[2] != d || (vn ? (r[0] != p || r[3] != p * d) : r[0] != p * d)) return 0;
+      }
+      return (int)d;
+    };
+    h->f_cn_uni = uniform(ft.cn_task, g->n_c, false);
+    h->f_vn_uni = uniform(ft.vn_task, g->n_v, true);
+  }
   h->f_nreg = nreg;
   h->f_dbuf = dbuf ? 1 : 0;
   h->f_lds = lds;

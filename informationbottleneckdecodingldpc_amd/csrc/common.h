@@ -21,6 +21,12 @@ constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, 
 #endif
 constexpr int kW = IBL_W;
 constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
+// IBL_LIGHT_W: dwords per lane and row of the variable pass's light items (degree <= kLightD):
+// IBL_W, or 4 for 1-KiB row segments per wave (chunks of 2048 codewords)
+#ifndef IBL_LIGHT_W
+#define IBL_LIGHT_W IBL_W
+#endif
+constexpr int kRowPad = 512 * (IBL_LIGHT_W > IBL_W ? IBL_LIGHT_W : IBL_W);   // row padding (codewords)
 constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item
 constexpr int kTbl = 8192;        // LDS bytes per IB lookup table (replicated over the 32 banks)
 // LDS table layout: 4 tables interleaved per 32-KiB region — byte (slot & 3) of the dword at row
@@ -117,6 +123,10 @@ struct IbFusedArgs {
   int32_t cn_nt, vn_nt, dec_nt, nreg;   // regions per pass image; nreg = table regions reserved in LDS
   int32_t dbuf;             // 1: two table sets of nreg regions (phase p reads set p & 1; the next phase's
                             // set is written during the current phase), no raw buffer
+  int32_t n_cn_nodes;
+  int32_t cn_uni, vn_uni;   // > 0: every task record is {64 t D, min(64, n - 64 t), D, ...} with this D
+                            // (single-degree side): computed from t instead of loaded (no scalar-load
+                            // wait, which also drains the wave's LDS queue, per task)
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, B, imax, half, match, out_dtype, aligned, ngroups;
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED): block 0's clock at every phase boundary of its
                             // first group, else nullptr

@@ -191,11 +191,18 @@ struct ItemBuf {
   int cwb;                 // first codeword of this lane
 };
 
+// Items of a phase: item = first + (pos - pos0) * nch + chunk (nch chunks of 512*W codewords per node)
+struct PhaseItems {
+  int first, pos0, nch;
+};
+
 template <class Buf, bool VN, bool GATHER>
-__device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, Buf& b) {
+__device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, Buf& b, const PhaseItems& pi) {
   constexpr int W = Buf::W, MAXD = Buf::kMax;
-  const int pos = __builtin_amdgcn_readfirstlane(item / a.nchunks);
-  const int chunk = __builtin_amdgcn_readfirstlane(item - pos * a.nchunks);
+  const int rel = item - pi.first;
+  const int q = __builtin_amdgcn_readfirstlane(rel / pi.nch);
+  const int chunk = __builtin_amdgcn_readfirstlane(rel - q * pi.nch);
+  const int pos = pi.pos0 + q;
   const int node = sload(a.info, 4 * pos);
   b.node = node;
   b.st = sload(a.info, 4 * pos + 1);
@@ -456,7 +463,7 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
                                          int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat,
-                                         uint64_t* trace_items) {
+                                         uint64_t* trace_items, const PhaseItems pi) {
   // always inlined: an out-of-line body would take the item by reference through scratch
   auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
     settle(cur);
@@ -494,25 +501,25 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb, Cc;
     int ia = item_of(take_ticket(ctr, lane));
     if (ia >= end) return;
-    fetch_item<Buf, VN, GATHER>(a, ia, lane, A);
+    fetch_item<Buf, VN, GATHER>(a, ia, lane, A, pi);
     int ib = item_of(take_ticket(ctr, lane));
-    fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb);
+    fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int ic = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ic, end - 1), lane, Cc);
+      fetch_item<Buf, VN, GATHER>(a, min(ic, end - 1), lane, Cc, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (ib >= end) break;
       ia = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ia, end - 1), lane, A);
+      fetch_item<Buf, VN, GATHER>(a, min(ia, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
       if (ic >= end) break;
       ib = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb);
+      fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(Cc);
       ++done;
@@ -522,18 +529,18 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb;
     int item = item_of(take_ticket(ctr, lane));
     if (item >= end) return;
-    fetch_item<Buf, VN, GATHER>(a, item, lane, A);
+    fetch_item<Buf, VN, GATHER>(a, item, lane, A, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int next = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (next >= end) break;
       item = next;
       next = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
@@ -552,10 +559,13 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   const int wpb = blockDim.x >> 6;
   // wave-uniform item counter: keeps the item loop, the degree switch and the graph-array loads scalar
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)), nw = gridDim.x * wpb;
-  const int heavy_end = a.n_heavy * a.nchunks, nitems = a.n_nodes * a.nchunks;
+  constexpr int W = rowW<MAXD>();
+  // the variable pass's light items may use wider rows (IBL_LIGHT_W) and hence fewer chunks per node
+  constexpr int LW = (VN && MAXD <= 8) ? IBL_LIGHT_W : W;
+  const int nch_l = LW == W ? a.nchunks : (a.B + 512 * LW - 1) / (512 * LW);
+  const int heavy_end = a.n_heavy * a.nchunks, nitems = heavy_end + (a.n_nodes - a.n_heavy) * nch_l;
   const bool do_par = !VN && !GATHER && a.unsat != nullptr;   // pass 0 (gather) has no syndrome
   bool unsat = false;
-  constexpr int W = rowW<MAXD>();
   // trace words written as they arise (start clock, items): values live across the whole pass cost
   // the MAXD=8 check node 2 spilled VGPRs
   uint64_t* trace_items = a.trace ? a.trace + 3 * gw + 2 : nullptr;
@@ -575,10 +585,10 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)
       ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
-                                                      trace_items);
+                                                      trace_items, PhaseItems{0, 0, a.nchunks});
     else
-      ib_phase<ItemBuf<kLightD, W>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2)>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
-                                                   unsat, trace_items);
+      ib_phase<ItemBuf<kLightD, LW>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2)>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
+                                                   unsat, trace_items, PhaseItems{heavy_end, a.n_heavy, nch_l});
   }
   if (a.trace && lane == 0) {
     a.trace[3 * gw + 1] = __builtin_readcyclecounter();
@@ -748,10 +758,17 @@ struct VnTask {
 template <int MAXD>
 __device__ __forceinline__ void fetch_vn_task(const IbFusedArgs& a, const uint32_t* chg, int t, int lane,
                                               VnTask<MAXD>& v) {
-  v.pos = sload(a.vn_task, 4 * t);
-  v.cnt = sload(a.vn_task, 4 * t + 1);
-  v.d = sload(a.vn_task, 4 * t + 2);
-  v.sf = sload(a.vn_task, 4 * t + 3);
+  if (a.vn_uni) {
+    v.pos = 64 * t;
+    v.cnt = min(64, a.n_v - v.pos);
+    v.d = a.vn_uni;
+    v.sf = v.pos * v.d;
+  } else {
+    v.pos = sload(a.vn_task, 4 * t);
+    v.cnt = sload(a.vn_task, 4 * t + 1);
+    v.d = sload(a.vn_task, 4 * t + 2);
+    v.sf = sload(a.vn_task, 4 * t + 3);
+  }
   const int li = min(lane, v.cnt - 1);
   v.chw = chg[v.pos + li];
 #pragma unroll
@@ -935,7 +952,16 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     for (;;) {
       const int t = take_ticket(c, lane);
       if (t >= a.n_cn_tasks) break;
-      const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
+      int first, cnt, d;
+      if (a.cn_uni) {
+        d = a.cn_uni;
+        first = 64 * t * d;
+        cnt = min(64, a.n_cn_nodes - 64 * t);
+      } else {
+        first = sload(a.cn_task, 4 * t);
+        cnt = sload(a.cn_task, 4 * t + 1);
+        d = sload(a.cn_task, 4 * t + 2);
+      }
       if (lane < cnt) {
         switch (d) {
 #define X(D) case D: if constexpr (D <= CMAX) fused_cn_dword<D>(msg, first, cnt, lane, lane4, a, do_par, vmask, unsat); break;

@@ -26,6 +26,9 @@ VARIANTS = {
     "mix3": ["IBL_MIX=3"],
     # two light variable items in flight per wave (ping-pong) instead of three
     "ld2": ["IBL_LIGHT_DEPTH=2"],
+    # variable pass light items with 1-KiB row segments per wave (4 dwords per lane), 3 / 2 in flight
+    "lw4": ["IBL_LIGHT_W=4"],
+    "lw4d2": ["IBL_LIGHT_W=4", "IBL_LIGHT_DEPTH=2"],
     # plain (cached) variable-pass row accesses instead of the default nontemporal ones
     "nt0": ["IBL_NT=0"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
