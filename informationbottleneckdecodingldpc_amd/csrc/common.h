@@ -21,10 +21,12 @@ constexpr int kChunk = 256;       // codewords per wave item (fp32: 4 per lane, 
 #endif
 constexpr int kW = IBL_W;
 constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
-// IBL_LIGHT_W: dwords per lane and row of the variable pass's light items (degree <= kLightD):
-// IBL_W, or 4 for 1-KiB row segments per wave (chunks of 2048 codewords)
+// IBL_LIGHT_W: dwords per lane and row of the variable pass's light items (degree <= kLightD; the
+// MAXD=8 bodies): 4 = 1-KiB row segments per wave, chunks of 2048 codewords. A/B on one box (DVB-S2
+// B=8192, 2 reps, tools/r03f.sh): light W=2 with 3 items in flight VN 0.4737 ms / 168.6k cw/s, W=4
+// with 3 in flight 0.4594 / 170.7k, W=4 with 2 in flight 0.4583 / 170.9k (the default)
 #ifndef IBL_LIGHT_W
-#define IBL_LIGHT_W IBL_W
+#define IBL_LIGHT_W 4
 #endif
 constexpr int kRowPad = 512 * (IBL_LIGHT_W > IBL_W ? IBL_LIGHT_W : IBL_W);   // row padding (codewords)
 constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item

@@ -457,8 +457,9 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 // DEPTH: items in flight per wave (2 = ping-pong; 3 for the variable pass's light phase, whose items
 // are HBM-bound: A/B on one box, DVB-S2 B=8192, 2 reps: depth 2 VN 0.4618 ms / 174.1k cw/s, depth 3
 // 0.4570 ms / 174.7k)
+// (with the 1-KiB light rows of IBL_LIGHT_W = 4, depth 2 and 3 measure the same; 2 is the default)
 #ifndef IBL_LIGHT_DEPTH
-#define IBL_LIGHT_DEPTH 3
+#define IBL_LIGHT_DEPTH 2
 #endif
 template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,

@@ -24,8 +24,9 @@ VARIANTS = {
     "mix1": ["IBL_MIX=1"],
     "mix2": ["IBL_MIX=2"],
     "mix3": ["IBL_MIX=3"],
-    # two light variable items in flight per wave (ping-pong) instead of three
-    "ld2": ["IBL_LIGHT_DEPTH=2"],
+    # three light variable items in flight per wave instead of two; round-2 light rows (W=2, depth 3)
+    "ld3": ["IBL_LIGHT_DEPTH=3"],
+    "lw2": ["IBL_LIGHT_W=2", "IBL_LIGHT_DEPTH=3"],
     # variable pass light items with 1-KiB row segments per wave (4 dwords per lane), 3 / 2 in flight
     "lw4": ["IBL_LIGHT_W=4"],
     "lw4d2": ["IBL_LIGHT_W=4", "IBL_LIGHT_DEPTH=2"],
