@@ -135,9 +135,9 @@ def emit_body(kind, D, S, L, NC):
     for j in col_in:
         for s in range(S):
             lines.append(f"  const uint64_t C{j}_{s} = colf(nib(in[{j}], k0 + {s}), cb[{j - (D - NC)}]);")
-    if kind == "vn":
+    if kind == "vn":   # channel nibble as a row term: luc merges it with a column term in one v_lshl_or
         for s in range(S):
-            lines.append(f"  const uint32_t c_{s} = nib(chw, k0 + {s}) << 11;")
+            lines.append(f"  const uint32_t c_{s} = nib(chw, k0 + {s});")
 
     def name(cid, k, s):
         return f"v_{cid}_{k}_{s}"
@@ -158,7 +158,7 @@ def emit_body(kind, D, S, L, NC):
             op, j, sl, _ = step
             for s in range(S):
                 if op == "c":
-                    expr = f"lu(c_{s} + q{j}_{s}, {sl})"
+                    expr = f"luc(c_{s}, q{j}_{s}, {sl})"
                 else:
                     prev = start_val(c, s) if k == 0 else name(cid, k - 1, s)
                     expr = f"csel(C{j}_{s}, {prev} << 2)" if is_col(step) else f"luc({prev}, q{j}_{s}, {sl})"
