@@ -128,10 +128,12 @@ def emit_body(kind, D, S, L, NC):
     lines = []
     u8_in = sorted({s[1] for c in chains for s in c["steps"] if not is_col(s)})
     col_in = sorted({s[1] for c in chains for s in c["steps"] if is_col(s)})
+    if D - 1 in u8_in:   # column base of the last input: final-table slot added once, not per codeword
+        lines.append("  const uint32_t lane4f = lane4 + fbase;")
     for j in u8_in:
         for s in range(S):
-            extra = " + fbase" if j == D - 1 else ""
-            lines.append(f"  const uint32_t q{j}_{s} = qidx(nib(in[{j}], k0 + {s}), lane4){extra};")
+            base = "lane4f" if j == D - 1 else "lane4"
+            lines.append(f"  const uint32_t q{j}_{s} = qidx(nib(in[{j}], k0 + {s}), {base});")
     for j in col_in:
         for s in range(S):
             lines.append(f"  const uint64_t C{j}_{s} = colf(nib(in[{j}], k0 + {s}), cb[{j - (D - NC)}]);")
