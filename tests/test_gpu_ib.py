@@ -45,6 +45,10 @@ CASES = [
     ("reg", 5, 511, True, True),
     ("dvb", 4, 6, True, False),
     ("dvb", 3, 2, False, True),
+    # B past one 2048-codeword light-row chunk (the variable pass's degree <= 4 items read 1-KiB row
+    # segments; rows are padded to 2048 codewords): a full chunk plus a ragged one
+    ("reg", 4, 3000, True, False),
+    ("dvb", 2, 2100, False, True),
 ]
 
 
