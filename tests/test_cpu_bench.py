@@ -66,3 +66,16 @@ def test_numpy_host_baseline_workers(tmp_path):
     for k in range(6):
         np.testing.assert_array_equal(outs[:, k], ref.decode(x[:, k]))
     assert per_core > 0 and agg > 0 and wall > 0
+
+
+def test_committed_pmc_traffic_feeds_the_headline(dvb):
+    """profiles/pmc_traffic.json (bench.py's default --pmc) is in the schema bench.py reads, so the
+    headline line carries the measured per-launch HBM bytes of its dominant kernel (roofline.traffic),
+    and they lie within 2 % of the stored algorithmic bytes (no wasted re-reads)."""
+    import os
+    g, B = dvb, 8192
+    pmc = os.path.join(os.path.dirname(bench.__file__), "profiles", "pmc_traffic.json")
+    r = bench.roofline(_args(pmc=pmc), g, g.n_v, B, 50, 1, 0.5, "u4", True, False,
+                       cn_avg=0.464, vn_avg=0.458, cn_ms=0.464 * 50, vn_ms=0.458 * 49, cn_n=50, vn_n=49, dec=None)
+    assert r["traffic"] is not None
+    assert abs(r["traffic"] / r["bytes_per_launch"] - 1) < 0.02
