@@ -58,7 +58,7 @@ def parse():
     p.add_argument("--path", "--float-path", dest="path", choices=["auto", "passes", "fused"], default="auto",
                    help="fused on-chip kernel when the code fits in LDS (auto), or per-pass launches")
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
-    p.add_argument("--cpu-procs", type=int, default=0, help="numpy host baseline processes (0 = min(16, host CPUs))")
+    p.add_argument("--cpu-procs", type=int, default=0, help="CPU-baseline processes / oracle threads (0 = this job's CPU share, bench.cpu_share())")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     a = p.parse_args()
@@ -86,8 +86,25 @@ def make_code(name):
 
 
 def bytes_per_cw(n_e: int, n_v: int, imax: int, w: int) -> int:
-    """i_max·(4·E·w_m + N·w_c) + N·(w_c + w_o)."""
+    """SURVEY §8(d)'s fixed reporting width: i_max·(4·E·w_m + N·w_c) + N·(w_c + w_o) — the u8-equivalent
+    figure (reported as *_u8_equivalent; the 4-bit and fused paths never move these bytes)."""
     return imax * (4 * n_e * w + n_v * w) + n_v * (w + w)
+
+
+def moved_bytes_per_cw(n_e: int, n_v: int, imax: int, path: str, ws: float, w_in: int, w_out: int,
+                       w_stage: float = 1) -> float:
+    """HBM bytes one codeword's decode moves at the widths the kernels store (fixed iterations).
+
+    per-pass ("passes"): stage (read N·w_in, write N·ws); check pass 0 (IB: gathers the staged channel per
+    edge and writes E; float: send reads N and writes E); i_max−1 loop iterations of variable pass (read
+    E+N, write E) + check pass (read E, write E); decision (read E+N, write N·w_out) — messages at ws bytes.
+    fused ("fused"): channel in (N·w_in), the transposed staging copy (N·w_stage written and read: u8 for IB,
+    the float width for min-sum / BP), output out (N·w_out); the messages never leave LDS."""
+    E, N = n_e, n_v
+    if path == "fused":
+        return N * w_in + 2 * N * w_stage + N * w_out
+    return (N * w_in + N * ws + (E + N if ws >= 4 else 2 * E) * ws
+            + (imax - 1) * (4 * E + N) * ws + (E + N) * ws + N * w_out)
 
 
 LDS_CLK_GHZ = 2.4          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
@@ -205,6 +222,40 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
     return roof
 
 
+def aggregate_rate(B: int, steps: int, elapsed_local: float) -> dict:
+    """Whole-job rate over the ranks of the process group: world·B·steps ÷ the slowest rank's timed region
+    (max over ranks), plus what the group was (backend, world size) and the per-rank rates (min / max), so a
+    multi-GPU record shows which backend and how many ranks produced it."""
+    import torch.distributed as dist
+
+    from informationbottleneckdecodingldpc_amd import distributed
+    on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size() if on else 1
+    mx = distributed.allreduce_max(elapsed_local)
+    mn = -distributed.allreduce_max(-elapsed_local)
+    return {"value": world * B * steps / mx, "elapsed_max_s": mx, "world_size": world,
+            "backend": dist.get_backend() if on else "none",
+            "per_rank_codewords_per_s": {"min": B * steps / mx, "max": B * steps / mn}}
+
+
+def cpu_share() -> int:
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 quota and by the job's
+    OMP_NUM_THREADS (the GPU box grants one GPU's job a 16-CPU share of a many-core host and says so there;
+    os.cpu_count() reports the whole host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, -(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as fh:
@@ -274,9 +325,12 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
     from oracle import oracle
     host = (lambda S_: src[:, :S_].cpu().numpy().astype(np.int32 if a.kind == "ib" else np.float64))  # noqa: E731
     ncpu = os.cpu_count() or 1
+    share = cpu_share()
+    proj_note = (f"per_core x host_cpus ({ncpu}); projected, not measured: this job's CPU share is {share} "
+                 f"(affinity / cgroup quota / OMP_NUM_THREADS), and the box runs at most that many workers")
     if a.kind == "ib" and a.code == "regular" and not match:
         # the reference's own CPU path: numpy decode_on_host (regular class), one codeword per call
-        procs = a.cpu_procs or min(16, ncpu)
+        procs = a.cpu_procs or share
         tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
         per_cw_s = 0.0028 * I                         # ~2.8 ms per (3,6) N=8000 iteration per core
         S = int(min(B, a.cpu_sample, max(procs, 30.0 / per_cw_s)))   # ~30 s of CPU work
@@ -286,25 +340,32 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
         ref, per_core, agg, wall = numpy_host_baseline(g, tbh, x, I, True, procs)
         same = bool(np.array_equal(ref, out[:, :S].cpu().numpy().astype(np.int64)))
         return {"value": round(agg, 3), "unit": "codewords/s", "cores": procs, "kind": "port",
-                "per_core": round(per_core, 3), "cpu_model": _cpu_model(), "host_cpus": ncpu,
+                "per_core": round(per_core, 3), "cpu_model": _cpu_model(), "host_cpus": ncpu, "cpu_share": share,
+                "all_cores_projected": {"value": round(per_core * ncpu, 3), "note": proj_note},
                 "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, no matching, fixed iterations; "
                           f"the reference's numpy decode_on_host (Discrete_LDPC_decoder_class, restated in "
                           f"oracle/host_numpy.py, bit-identical to the reference's outputs), one codeword per call, "
                           f"{procs} single-threaded processes, {wall:.1f} s wall; outputs equal GPU: {same}"}
-    nthreads = min(16, ncpu)
+    nthreads = a.cpu_procs or share
     # bounded sample: a 16-codeword calibration run sizes the measured sample to ~12 s of CPU work
     if a.kind == "ib":
         tbh = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
-        dec_cpu = lambda x: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nthreads)  # noqa: E731
+        dec_cpu = lambda x, nt=nthreads: oracle.ib_decode(g, tbh, x, match=match, early_stop=False, nthreads=nt)  # noqa: E731
     elif a.kind == "minsum":
         # fp32 min-sum restated in IEEE single (oracle/float_oracle.inc): the same arithmetic as the GPU
-        dec_cpu = lambda x: oracle.float32_decode(g, I, x.astype(np.float32), nthreads=nthreads)  # noqa: E731
+        dec_cpu = lambda x, nt=nthreads: oracle.float32_decode(g, I, x.astype(np.float32), nthreads=nt)  # noqa: E731
     else:
-        dec_cpu = lambda x: oracle.float_decode(g, 1, I, x, early_stop=False, nthreads=nthreads)  # noqa: E731
+        dec_cpu = lambda x, nt=nthreads: oracle.float_decode(g, 1, I, x, early_stop=False, nthreads=nt)  # noqa: E731
     S0 = min(16, B)
     t1 = time.perf_counter()
     dec_cpu(host(S0))
     cal = time.perf_counter() - t1
+    # one thread: the per-core rate (about 2 s of work)
+    S1 = int(max(1, min(S0, 2.0 * S0 / max(cal * nthreads, 1e-3))))
+    x1 = host(S1)
+    t1 = time.perf_counter()
+    dec_cpu(x1, 1)
+    per_core = S1 / (time.perf_counter() - t1)
     S = int(max(S0, min(B, a.cpu_sample, S0 * 12.0 / max(cal, 1e-3))))
     x_cpu = host(S)
     t1 = time.perf_counter()
@@ -327,7 +388,8 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
                 f"paths are broken, SURVEY App. C3); GPU fp32 APP LLRs within 1e-5 rel + 1e-4: {within:.6f}, "
                 f"hard decisions equal: {agree:.6f}")
     return {"value": round(S / cpu_s, 3), "unit": "codewords/s", "cores": nthreads, "kind": "port",
-            "cpu_model": _cpu_model(), "host_cpus": ncpu,
+            "per_core": round(per_core, 4), "cpu_model": _cpu_model(), "host_cpus": ncpu, "cpu_share": share,
+            "all_cores_projected": {"value": round(per_core * ncpu, 3), "note": proj_note},
             "sample": f"{S} of the benchmark's codewords, {code_name}, i_max={I}, fixed iterations; {what}; "
                       f"{cpu_s:.1f} s wall"}
 
@@ -408,16 +470,16 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    elapsed_local = time.perf_counter() - t0
     timing_on(False)
     cn_ms, cn_n, vn_ms, vn_n = timing_read()
-    elapsed = distributed.allreduce_max(elapsed)
 
     # errors of the decoded batch (sanity: counted on device, outside the timed region)
     errs = int(engine.count_below(out, g.data_len, 8 if a.kind == "ib" else 0.0).item())
     tot = distributed.allreduce_counts({"errors": errs, "bits": g.data_len * B})
 
-    value = world * B * a.steps / elapsed
+    agg = aggregate_rate(B, a.steps, elapsed_local)
+    elapsed, value = agg["elapsed_max_s"], agg["value"]
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
     fused = dec.fused
@@ -429,6 +491,8 @@ def main():
     if a.kind == "ib":
         dtype = fmt
     roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec)
+    # HBM bytes the decode moves per codeword at the stored widths (channel in, output out: u8 for IB, fp32 float)
+    moved = moved_bytes_per_cw(g.n_e, n_v, I, "fused" if fused else "passes", ws, w, w, w_stage=w)
     cpu = None
     code_name, code_desc = CODES[a.code]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -459,8 +523,16 @@ def main():
                                    f", fixed iterations",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
-            "hbm_gbps_algorithmic": round(value * bpc / 1e9, 1),
-            "bytes_per_codeword": bpc,
+            "hbm_gbps_algorithmic": round(value * moved / 1e9, 1),
+            "bytes_per_codeword": int(round(moved)),
+            "hbm_gbps_u8_equivalent": round(value * bpc / 1e9, 1),
+            "bytes_per_codeword_u8_equivalent": bpc,
+            "hbm_note": ("hbm_gbps_algorithmic = codewords/s x the bytes the kernels move per codeword at their stored "
+                         f"widths ({fmt} messages{', fused on-chip: channel in + output out only' if fused else ''}); "
+                         "*_u8_equivalent = SURVEY §8(d)'s fixed 1-byte reporting width, not bytes moved"),
+            "dist": {k: (round(v, 6) if isinstance(v, float) else
+                         ({a_: round(b_, 1) for a_, b_ in v.items()} if isinstance(v, dict) else v))
+                     for k, v in agg.items() if k != "value"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "decoded_bit_errors": tot["errors"], "decoded_bits": tot["bits"],

@@ -781,7 +781,9 @@ int fused_setup(ibl_float* h) {
   size_t lds = (size_t)(E + g->n_v) * 16 + 16;
   // variable-edge slot indices as u16 in LDS when they fit (E < 65536 and the space is there)
   const size_t lds16 = (size_t)(E + g->n_v) * 16 + 16 + (size_t)E * 2;
-  const bool slot16 = E < 65536 && lds16 <= (size_t)kLdsBytes;
+  // IBL_FUSED_SLOT16=0 forces the global int32 slot reads (test hook: tests/test_gpu_float.py runs that path)
+  const char* s16e = getenv("IBL_FUSED_SLOT16");
+  const bool slot16 = E < 65536 && lds16 <= (size_t)kLdsBytes && !(s16e && s16e[0] == '0');
   if (slot16) lds = lds16;
   int min_dc = 1 << 30;
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);

@@ -138,6 +138,11 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put
     // (sign() = 0 kills the reference's fold) makes mn1 = 0, so every other output is +-0 as there; the
     // zero's own output is the others' min. Running (mn1, mn2) with v_min / v_med3 on |m| (abs is an
     // input modifier), signs XORed as bits: ~2.5 VALU per input and 4 per output.
+    // Assumption (the only case where the closed form and the fold differ): no product m*t of the fold
+    // underflows to 0 (sign(0) = 0 would zero the reference's output). Every message is a sum of channel
+    // LLRs and selected messages, so each nonzero one is a multiple of the ulp q of the smallest nonzero
+    // |channel LLR|; with that LLR >= 2^-50 (fp32; 2^-450 fp64) every product is >= 2^-146 and none
+    // underflows (tests/test_gpu_float.py::test_float32_minsum_tiny_llrs runs that boundary bit-exactly).
     using Bt = Bits<F>;
     using U = typename Bt::U;
     F mn1[N], mn2[N];
@@ -846,7 +851,7 @@ static const void* fl_fused_kernel(int kind, int prec, int maxd) {
 hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block) {
   const void* f = fl_fused_kernel(kind, prec, maxd);
   *block = fl_block(0, kind, prec, maxd);
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
 }

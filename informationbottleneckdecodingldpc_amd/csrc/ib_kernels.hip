@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(256) void ib_stage_t(const void* ch, int dtype, int
     // u8 rows whose 4-codeword words are aligned (B % 4 == 0) load one dword per word
     constexpr int kPer = P * 2 * G / 256;
     uint32_t w[kPer];
-    const bool words = dtype == kU8 && (B & 3) == 0;
+    const bool words = dtype == kU8 && (B & 3) == 0 && (reinterpret_cast<uintptr_t>(ch) & 3) == 0;
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = threadIdx.x + it * 256;
@@ -1345,14 +1345,14 @@ hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t ld
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu) {
   if (which == 0) {  // both variants must accept the LDS size; report the non-gather one
     for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>}) {
-      hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
       if (e != hipSuccess) return e;
     }
   }
   const void* f = which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
                 : which == 1 ? (maxd <= 8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>)
                              : (const void*)ib_dec_fast;
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   hipFuncAttributes fa;
   e = hipFuncGetAttributes(&fa, f);
@@ -1399,7 +1399,10 @@ hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, i
 }
 hipError_t ib_fused_occupancy(int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block, size_t* private_bytes) {
   const void* f = ib_fused_kernel(cmax, vmax);
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // the dynamic-LDS cap is an attribute of the kernel instantiation, shared by every decoder that launches it:
+  // set it to the CU's whole LDS (here and in the other *_occupancy functions), never to one decoder's size,
+  // or a smaller decoder created later would lower the cap an earlier, larger one launches with
+  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   hipFuncAttributes fa;
   if ((e = hipFuncGetAttributes(&fa, f)) != hipSuccess) return e;

@@ -48,6 +48,10 @@ def init_from_env(backend: str | None = None) -> Tuple[int, int, torch.device]:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or ("nccl" if use_gpu else "gloo")
+        if backend == "gloo" and use_gpu and os.environ.get("IBL_SHARE_DEVICE") != "1":
+            # one GPU per rank is the production layout: its collectives belong on RCCL over xGMI
+            raise RuntimeError("refusing the gloo backend with one GPU per rank: use nccl (RCCL), or set "
+                               "IBL_SHARE_DEVICE=1 for a shared-device rehearsal")
         kwargs = {"device_id": device} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
     return rank, world, device

@@ -63,6 +63,52 @@ def test_gloo_world2_broadcast_shard_allreduce():
     assert m0 == m1 == 2.5
 
 
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import bench
+    from informationbottleneckdecodingldpc_amd import distributed
+    distributed.init_from_env(backend="gloo")
+    try:
+        q.put((rank, bench.aggregate_rate(1000, 4, 2.0 if rank == 0 else 4.0)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_aggregation():
+    """bench.py's whole-job rate: world·B·steps ÷ the slowest rank's time, and the record names the backend,
+    the world size and the per-rank rates."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    r = res[0]
+    assert r["value"] == 2 * 1000 * 4 / 4.0 and r["elapsed_max_s"] == 4.0
+    assert r["world_size"] == 2 and r["backend"] == "gloo"
+    assert r["per_rank_codewords_per_s"] == {"min": 1000.0, "max": 2000.0}
+
+
+def test_gloo_refused_with_one_gpu_per_rank(monkeypatch):
+    import torch
+
+    from informationbottleneckdecodingldpc_amd import distributed
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.delenv("IBL_SHARE_DEVICE", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
+    with pytest.raises(RuntimeError, match="refusing the gloo backend"):
+        distributed.init_from_env(backend="gloo")
+
+
 @pytest.mark.parametrize("total,world", [(64 * 1024, 8), (10, 3), (7, 8), (0, 2)])
 def test_shard_range_partitions(total, world):
     spans = [shard_range(total, r, world) for r in range(world)]

@@ -2,6 +2,7 @@
 symbols and host-only index construction, the drop-in classes' set-up, and the fail-loudly rule."""
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -181,3 +182,18 @@ def test_decode_kernels_have_no_private_segment(lib):
                 seen[m.group(1)] = int(p.group(1))
     assert len(seen) >= 20, seen
     assert {k: v for k, v in seen.items() if v} == {}
+
+
+def test_generated_schedules_are_current():
+    """csrc/ib_sched.inc is exactly what tools/gen_sched.py emits with the parameters named in its first
+    line (a hand edit or a stale regeneration fails here, not only in the GPU bit-exact tests)."""
+    import subprocess
+    inc = os.path.join(ROOT, "informationbottleneckdecodingldpc_amd", "csrc", "ib_sched.inc")
+    with open(inc) as fh:
+        text = fh.read()
+    first = text.splitlines()[0]
+    assert first.startswith("// GENERATED by tools/gen_sched.py")
+    args = first[len("// GENERATED by tools/gen_sched.py"):].split("--")[0].split()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sched.py"), *args],
+                       capture_output=True, text=True, check=True)
+    assert r.stdout == text

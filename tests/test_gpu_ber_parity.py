@@ -86,6 +86,48 @@ def test_ib_ber_curve_equals_oracle(name, imax, B, max_blocks, start, stop, step
     assert ref[2][0] > ref[2][-1]          # the curve falls over the sweep
 
 
+@pytest.mark.parametrize("prec", [torch.float64, torch.float32])
+def test_bp_ber_curve_c5_dvbs2(prec, dvb_H):
+    """BASELINE C5 (DVB-S2 BP, i_max=100, Eb/N0 sweep) through the reference-named BP class and the BER
+    driver, as ``WLAN/BER_simulation_OpenCL_quant_BP.py:105-110`` calls it (``quantize_direct_OpenCL_LLR`` ->
+    ``decode_OpenCL_belief_propagation`` -> ``return_errors_all_zero``), replayed on the fp64 oracle
+    (``oracle.float_decode(kind=BP)``, early stop on) over the identical Philox channel stream.
+
+    Bar: identical Eb/N0 points and block counts (the state machine), and per-point error counts
+    identical to the oracle's — for the fp64 build always; for the fp32 build where the two
+    trajectories agree (every converged codeword does: H5, test_gpu_float.py), otherwise within the
+    stated bound |e32 - e64| <= 4 sqrt(e32 + e64 + 1) per point (a paired-difference bound, ~6e-5
+    false-alarm rate under 'same decoder statistic'). Measured on MI355X: identical counts at every
+    point for both builds (DESIGN.md §Float parity)."""
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    g = graph.build_graph(dvb_H)
+    B, imax = 16, 100
+    bp = BeliefPropagationDecoderClassIrregular(dvb_H, imax, 16, B, precision=prec)
+    cfg = BERConfig(EbN0_dB_start=0.6, EbN0_dB_max_value=1.4, EbN0_dB_normal_stepwidth=0.4,
+                    EbN0_dB_small_stepwidth=0.2, target_error_rate=1e-9, min_errors=10 ** 9, msg_at_time=B,
+                    max_blocks=32, seed=23, llr_dtype=prec)
+    r = run_ber(bp, cfg)
+    np_dt = np.float64 if prec == torch.float64 else np.float32
+
+    def decode(cl, q):
+        llr = q.output_LLRs.astype(np_dt)[cl].astype(np.float64)   # the build's input LLRs, exactly
+        return oracle.float_decode(g, oracle.BP, imax, llr, early_stop=True)
+    ref = _replay(cfg, g.n_v, bp.data_len, float(bp.R_c), decode, lambda out, dl: float((out[:dl] < 0).sum()))
+    ebn0, ber, errs, blks = ref
+    np.testing.assert_allclose(r.EbN0_dB_vector, ebn0, rtol=0, atol=1e-12)
+    assert len(ebn0) >= 3 and r.blocks == blks
+    got = [int(e) for e in r.errors]
+    want = [int(e) for e in errs]
+    print(f"BP {prec}: points {list(ebn0)} errors gpu {got} oracle {want}")
+    if prec == torch.float64:
+        assert got == want
+        np.testing.assert_array_equal(r.BER_vector, ber)
+    else:
+        for a_, b_ in zip(got, want):
+            assert abs(a_ - b_) <= 4 * np.sqrt(a_ + b_ + 1), (got, want)
+    assert want[0] > want[-1]              # the curve falls over the sweep
+
+
 def test_minsum_fp32_ber_curve_equals_oracle():
     """BASELINE C3's code and decoder (WLAN N=1944, min-sum fp32, fused on-chip path) with the
     channel's float32 cluster LLRs: the BER curve equals the fp32 oracle's."""

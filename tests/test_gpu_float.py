@@ -234,6 +234,38 @@ def test_dropin_min_sum_and_bp(wlan_H):
     assert hd.shape == (g.n_v,)
 
 
+@pytest.mark.parametrize("prec", [torch.float64, torch.float32])
+@pytest.mark.parametrize("ebn0", [0.8, 1.4])
+def test_dropin_bp_c5_vs_oracle(dvb_H, prec, ebn0):
+    """The reference-named BP class on C5's code (DVB-S2, i_max=100), as the BP BER driver calls it
+    (WLAN/BER_simulation_OpenCL_quant_BP.py:105-110: decode_OpenCL_belief_propagation with early stop,
+    then return_errors_all_zero): APP LLRs vs the fp64 oracle (fp64 build 1e-9, fp32 build SURVEY H5 with
+    no hard flips) and the error count equal to the oracle's (bp_decoder_irreg.py:221-295)."""
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    g = graph.build_graph(dvb_H)
+    B = 8
+    llr = _llrs(g, B, ebn0, seed=int(ebn0 * 10) + 3)
+    if prec == torch.float32:
+        llr = llr.astype(np.float32).astype(np.float64)     # the fp32 build's inputs, exactly
+    bp = BeliefPropagationDecoderClassIrregular(dvb_H, 100, 16, B, precision=prec)
+    assert bp.data_len == 32399                             # reference R_c quirk (SURVEY App. C11)
+    bp.init_OpenCL_decoding(B)
+    ref = oracle.float_decode(g, oracle.BP, 100, llr, early_stop=True)
+    buf = bp.decode_OpenCL_belief_propagation(torch.from_numpy(llr).to(DEV).to(prec), buffer_in=True,
+                                              return_buffer=True)
+    assert buf.dtype == prec and tuple(buf.shape) == llr.shape
+    out = buf.double().cpu().numpy()
+    if prec == torch.float64:
+        np.testing.assert_allclose(out, ref, rtol=0, atol=1e-9)
+    else:
+        bad = _h5(out, ref)
+        assert bad.sum() == 0, f"{bad.sum()} LLRs outside H5, max |x-y| {np.abs(out - ref).max():.3e}"
+        assert _hard_flips(out, ref) == 0
+    assert bp.return_errors_all_zero(buf) == float((ref[:bp.data_len] < 0).sum())
+    host = bp.decode_OpenCL_belief_propagation(llr)         # host ndarray in and out
+    np.testing.assert_array_equal(host.astype(np.float64), out)
+
+
 def test_count_below_matches_numpy(eng):
     x = torch.randn(513, 77, device=DEV)
     assert int(eng.count_below(x, 300, 0.0).item()) == int((x[:300] < 0).sum().item())
@@ -288,3 +320,34 @@ def test_fused_path_selection(eng, wlan_H, dvb_H):
     from informationbottleneckdecodingldpc_amd._lib import IBLError
     with pytest.raises(IBLError):
         eng.FloatDecoder(D, 0, 5, 16, path="fused")
+
+
+@pytest.mark.parametrize("path", ["auto", "passes"])
+def test_float32_minsum_tiny_llrs(eng, wlan_H, path):
+    """The closed-form min-sum check node (float_kernels.hip fl_cn_body) equals the reference fold
+    t = sgn(m t) min(|t|, |m|) as long as no product m t underflows; scaling the quantised LLRs by 2^-50 (the
+    boundary stated there: every nonzero message stays a multiple of the smallest LLR's ulp, so products stay
+    >= 2^-146) keeps the fp32 GPU decode bit-exact with the literal fp32 oracle fold."""
+    g = graph.build_graph(wlan_H)
+    llr = _llrs(g, 64, 1.5, seed=17).astype(np.float32)
+    mn = float(np.abs(llr[llr != 0]).min())
+    llr = llr * np.float32(2.0 ** (-50 - int(np.floor(np.log2(mn)))))      # exact power-of-two scaling
+    assert 2.0 ** -50 <= np.abs(llr[llr != 0]).min() < 2.0 ** -49
+    ref = oracle.float32_decode(g, 20, llr)
+    out, _ = _gpu(eng, g, oracle.MINSUM, 20, llr, torch.float32, False, path=path)
+    np.testing.assert_array_equal(out, ref.astype(np.float64))
+
+
+@pytest.mark.parametrize("prec", [torch.float32, torch.float64])
+def test_fused_global_slot_index_path(eng, monkeypatch, wlan_H, prec):
+    """The fused float kernel's fallback that reads variable-edge slot indices from global memory (taken when
+    the u16 copy does not fit in LDS; IBL_FUSED_SLOT16=0 forces it at create) equals the per-pass path."""
+    g = graph.build_graph(wlan_H)
+    G = eng.Graph(g, DEV)
+    llr = _llrs(g, 130, 2.0, seed=29)
+    monkeypatch.setenv("IBL_FUSED_SLOT16", "0")
+    fused, it_f = _gpu(eng, g, oracle.MINSUM, 12, llr, prec, True, graph_obj=G, path="fused")
+    monkeypatch.delenv("IBL_FUSED_SLOT16")
+    passes, it_p = _gpu(eng, g, oracle.MINSUM, 12, llr, prec, True, graph_obj=G, path="passes")
+    assert it_f == it_p
+    np.testing.assert_array_equal(fused, passes)

@@ -332,3 +332,39 @@ def test_full_size_dvbs2_decodes_all_zero(eng, dvb_H):
     out = dec.decode(ch, out_dtype=torch.uint8, early_stop=True, iters=it)
     errs = int(eng.count_below(out, g.data_len, 8).item())
     assert errs == 0
+
+
+def test_fused_lds_cap_survives_a_smaller_decoder(wlan_H):
+    """The fused kernel's dynamic-LDS cap belongs to the kernel instantiation: a large-LDS decoder (regular
+    (3,6) N=8000 with two table sets) created first, then a smaller one (WLAN) on the same instantiation, and
+    the first decodes again — bit-exact against the oracle."""
+    from informationbottleneckdecodingldpc_amd import codes, engine
+    g1 = graph.build_graph(codes.regular_code(8000, 3, 6, seed=0))
+    tb1 = tables.random_tables(16, 16, g1.d_c_max, g1.d_v_max, 6, seed=4)
+    big = engine.IBDecoder(engine.Graph(g1, DEV), tb1, False, 64, path="fused")
+    g2 = graph.build_graph(wlan_H)
+    tb2 = tables.random_tables(16, 16, g2.d_c_max, g2.d_v_max, 6, seed=5)
+    small = engine.IBDecoder(engine.Graph(g2, DEV), tb2, False, 64, path="fused")
+    x2 = np.random.default_rng(2).integers(0, 16, (g2.n_v, 64)).astype(np.int32)
+    o2 = small.decode(torch.from_numpy(x2).to(DEV), early_stop=False).cpu().numpy()
+    np.testing.assert_array_equal(o2, oracle.ib_decode(g2, tb2, x2, match=False))
+    x1 = np.random.default_rng(1).integers(0, 16, (g1.n_v, 64)).astype(np.int32)
+    o1 = big.decode(torch.from_numpy(x1).to(DEV), early_stop=False).cpu().numpy()
+    np.testing.assert_array_equal(o1, oracle.ib_decode(g1, tb1, x1, match=False))
+
+
+@pytest.mark.parametrize("path", ["fused", "passes"])
+def test_misaligned_u8_channel(eng, wlan_H, path):
+    """A contiguous u8 channel view at an odd byte offset (B % 4 == 0, so the staging kernels' dword path
+    would apply to an aligned pointer) decodes bit-exactly: the dword loads are taken only when aligned."""
+    g = graph.build_graph(wlan_H)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 5, seed=8)
+    B = 64
+    x = np.random.default_rng(6).integers(0, 16, (g.n_v, B)).astype(np.uint8)
+    buf = torch.zeros(g.n_v * B + 1, dtype=torch.uint8, device=DEV)
+    ch = buf[1:].view(g.n_v, B)
+    ch.copy_(torch.from_numpy(x).to(DEV))
+    assert ch.is_contiguous() and ch.data_ptr() % 4 == 1
+    dec = eng.IBDecoder(eng.Graph(g, DEV), tb, True, B, path=path)
+    out = dec.decode(ch, early_stop=False).cpu().numpy()
+    np.testing.assert_array_equal(out, oracle.ib_decode(g, tb, x, match=True))
