@@ -103,8 +103,8 @@ def test_bp_ber_curve_c5_dvbs2(prec, dvb_H):
     g = graph.build_graph(dvb_H)
     B, imax = 16, 100
     bp = BeliefPropagationDecoderClassIrregular(dvb_H, imax, 16, B, precision=prec)
-    cfg = BERConfig(EbN0_dB_start=0.6, EbN0_dB_max_value=1.4, EbN0_dB_normal_stepwidth=0.4,
-                    EbN0_dB_small_stepwidth=0.2, target_error_rate=1e-9, min_errors=10 ** 9, msg_at_time=B,
+    cfg = BERConfig(EbN0_dB_start=0.2, EbN0_dB_max_value=1.2, EbN0_dB_normal_stepwidth=0.25,
+                    EbN0_dB_small_stepwidth=0.125, target_error_rate=1e-9, min_errors=10 ** 9, msg_at_time=B,
                     max_blocks=32, seed=23, llr_dtype=prec)
     r = run_ber(bp, cfg)
     np_dt = np.float64 if prec == torch.float64 else np.float32
