@@ -16,6 +16,10 @@ ARCH = os.environ.get("IBLDPC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wno-unused-result", "-Wno-pass-failed"]
+# per-source flags. float_kernels: the float messages are never NaN (finite channel LLRs, every operation
+# keeps them finite), so the kernels run with the IEEE mode bit off: v_min_f32 / v_max_f32 then take their
+# (|x|-modified) inputs directly instead of quieting each through a v_max x, x first
+SRC_FLAGS = {"float_kernels.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"]}
 
 
 def _stale(out: str, deps) -> bool:
@@ -37,7 +41,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB
         s = os.path.join(CSRC, src)
         o = os.path.join(objdir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", s, "-o", o])
+            jobs.append([HIPCC, *FLAGS, *SRC_FLAGS.get(src, []), *[f"-D{d}" for d in defines], "-c", s, "-o", o])
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):

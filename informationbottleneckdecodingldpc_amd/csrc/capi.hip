@@ -763,7 +763,7 @@ namespace {
 struct FusedTasks {
   std::vector<int32_t> cn_task, vn_task, vn_node, vn_slot;
 };
-int build_fused_tasks(const ibl_graph* g, FusedTasks* ft);
+int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order);
 int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_task, int32_t** vn_node, int32_t** vn_slot) {
   int rc;
   if ((rc = dupload(cn_task, ft.cn_task.data(), ft.cn_task.size())) || (rc = dupload(vn_task, ft.vn_task.data(), ft.vn_task.size())) ||
@@ -796,7 +796,11 @@ int fused_setup(ibl_float* h) {
   }
   FusedTasks ft;
   int rc;
-  if ((rc = build_fused_tasks(g, &ft)) ||
+  // 16-byte slots (ds_read_b128 / ds_write_b128): the natural order (stable by degree) keeps a quasi-cyclic
+  // code's lanes on runs of consecutive slots, which conflict less than the dword-bank greedy order;
+  // IBL_FUSED_VORDER=1 selects the greedy order (A/B)
+  const char* voe = getenv("IBL_FUSED_VORDER");
+  if ((rc = build_fused_tasks(g, &ft, voe && voe[0] == '1')) ||
       (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
     return rc;
   const std::vector<int32_t>& cn_task = ft.cn_task;
@@ -813,8 +817,9 @@ int fused_setup(ibl_float* h) {
 
 // Check nodes sorted by degree (heaviest first, stable) and cut into tasks of up to 64 nodes of one
 // degree; edge k of lane i of a check task gets slot first + k*count + i. Variable nodes likewise;
-// vn_slot maps each variable edge (task-major, k*count + i) to the slot of the same edge.
-int build_fused_tasks(const ibl_graph* g, FusedTasks* ft) {
+// vn_slot maps each variable edge (task-major, k*count + i) to the slot of the same edge. bank_order
+// reorders the variables of each degree for conflict-free dword slot reads (below).
+int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order) {
   const int64_t E = g->n_e;
   std::vector<int32_t> tgt_vn((size_t)E);
   if (hipMemcpy(tgt_vn.data(), g->tgt_vn, sizeof(int32_t) * (size_t)E, hipMemcpyDeviceToHost) != hipSuccess)
@@ -853,7 +858,7 @@ int build_fused_tasks(const ibl_graph* g, FusedTasks* ft) {
     // a bank (slot mod 32). Greedily fill each 32-lane group with variables whose k-th slots hit banks
     // not yet used by the group at that k (scan window 256): the fused IB kernel's dword slots then read
     // (almost) conflict-free. Any order gives the same results.
-    for (size_t i0 = 0; i0 < ord.size();) {
+    for (size_t i0 = 0; bank_order && i0 < ord.size();) {
       const int32_t d = g->h_vn_deg[ord[i0]];
       size_t i1 = i0;
       while (i1 < ord.size() && g->h_vn_deg[ord[i1]] == d) ++i1;
@@ -924,7 +929,8 @@ int ib_fused_setup(ibl_ib* h) {
   }
   FusedTasks ft;
   int rc;
-  if ((rc = build_fused_tasks(g, &ft)) ||
+  const char* voe = getenv("IBL_FUSED_VORDER");
+  if ((rc = build_fused_tasks(g, &ft, !(voe && voe[0] == '0'))) ||
       (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
     return rc;
   h->f_ncn = (int32_t)(ft.cn_task.size() / 4);

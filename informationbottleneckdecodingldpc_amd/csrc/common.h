@@ -271,7 +271,7 @@ hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per
 // Largest private segment over the float kernels of (kind, prec, degrees); fused included when asked.
 hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, int fused_maxd, size_t* bytes,
                             const char** name);
-int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
+int fl_block(int which, int kind, int prec, int maxd, bool fused = false);  // threads per block of the float CN (0) / VN (1) kernels
 hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block);
 

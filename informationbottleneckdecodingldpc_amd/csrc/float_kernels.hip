@@ -58,6 +58,16 @@ template <> struct Bits<float> {
   __device__ static U of(float x) { return __float_as_uint(x); }
   __device__ static float from(U u) { return __uint_as_float(u); }
   __device__ static float med3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+  __device__ static float lo(float a, float b) { return fminf(a, b); }
+  __device__ static float hi(float a, float b) { return fmaxf(a, b); }
+  // the compiler keeps v_and_b32 + v_or_b32 for this (gfx9 VOP3 takes no literal): one v_and_or_b32 with
+  // the mask in an SGPR places a sign bit
+  __device__ static U and_or(U a, U k, U b) {
+    U r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    return r;
+  }
+  __device__ static U sign_mask() { return __builtin_amdgcn_readfirstlane(kSign); }
 };
 template <> struct Bits<double> {
   using U = uint64_t;
@@ -66,6 +76,10 @@ template <> struct Bits<double> {
   __device__ static double from(U u) { return __longlong_as_double((long long)u); }
   // median of (lo <= hi, c): max(lo, min(hi, c))
   __device__ static double med3(double lo, double hi, double c) { return fmax(lo, fmin(hi, c)); }
+  __device__ static double lo(double a, double b) { return fmin(a, b); }
+  __device__ static double hi(double a, double b) { return fmax(a, b); }
+  __device__ static U and_or(U a, U k, U b) { return (a & k) | b; }
+  __device__ static U sign_mask() { return kSign; }
 };
 
 __device__ __forceinline__ double boxplus(double a, double b, double lm) {
@@ -126,6 +140,33 @@ struct FlOut {
   }
 };
 
+// XOR of the inputs' sign bits for codeword s. Its sign bit is also
+// the syndrome parity of the inputs (calc_syndrome, kernels_min_and_BP.cl:206-227: parity of m < 0):
+// a check's inputs are never -0, since the staged channel holds no -0 (fl_stage*, which turn -0 into +0:
+// equal values) and a variable's output clamp(ch + sum) is -0 only if every addend is.
+template <typename F, int D>
+__device__ __forceinline__ typename Bits<F>::U sign_xor(const F (&m)[D][Vec<F>::N], int s) {
+  using Bt = Bits<F>;
+  typename Bt::U x = Bt::of(m[0][s]);
+#pragma unroll
+  for (int j = 1; j < D; ++j) x ^= Bt::of(m[j][s]);
+  return x;
+}
+
+// Syndrome parity of codeword s's inputs: the sign bit of sign_xor (degrees <= 8); larger degrees keep
+// the compare-and-mask form (lane masks in SGPRs), which needs no VGPR beside the 16 inputs.
+template <typename F, int D>
+__device__ __forceinline__ bool syndrome_bit(const F (&m)[D][Vec<F>::N], int s) {
+  if constexpr (D <= 8) {
+    return (sign_xor<F, D>(m, s) >> (8 * sizeof(F) - 1)) != 0;
+  } else {
+    bool p = false;
+#pragma unroll
+    for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
+    return p;
+  }
+}
+
 // Check-node body on the inputs m (min-sum or BP); put(w, o) receives output w (any order of w).
 template <int KIND, typename F, int D, class Put>
 __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put&& put) {
@@ -147,18 +188,18 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put
     using U = typename Bt::U;
     F mn1[N], mn2[N];
     U sg[N];
+    const U ks = Bt::sign_mask();
 #pragma unroll
     for (int s = 0; s < N; ++s) {
       const F a0 = fabs(m[0][s]), a1 = fabs(m[1][s]);
-      mn1[s] = fmin(a0, a1);
-      mn2[s] = fmax(a0, a1);
-      sg[s] = Bt::of(m[0][s]) ^ Bt::of(m[1][s]);
+      mn1[s] = Bt::lo(a0, a1);
+      mn2[s] = Bt::hi(a0, a1);
+      sg[s] = sign_xor<F, D>(m, s);
 #pragma unroll
       for (int j = 2; j < D; ++j) {
         const F x = fabs(m[j][s]);
         mn2[s] = Bt::med3(mn1[s], mn2[s], x);
-        mn1[s] = fmin(mn1[s], x);
-        sg[s] ^= Bt::of(m[j][s]);
+        mn1[s] = Bt::lo(mn1[s], x);
       }
     }
 #pragma unroll
@@ -166,7 +207,10 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put
 #pragma unroll
       for (int s = 0; s < N; ++s) {
         const F mag = (fabs(m[w][s]) == mn1[s]) ? mn2[s] : mn1[s];
-        o[s] = Bt::from(Bt::of(mag) | ((sg[s] ^ Bt::of(m[w][s])) & Bt::kSign));
+        const U sx = sg[s] ^ Bt::of(m[w][s]);
+        // degrees > 8 keep the compiler's form: the asm operand copies would push the 16-input body past
+        // the 128 VGPRs of a 1024-thread block
+        o[s] = Bt::from(D <= 8 ? Bt::and_or(sx, ks, Bt::of(mag)) : (sx & Bt::kSign) | Bt::of(mag));
       }
       put(w, o);
     }
@@ -252,12 +296,7 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
   }
   if (do_par) {
 #pragma unroll
-    for (int s = 0; s < N; ++s) {
-      bool p = false;
-#pragma unroll
-      for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
-      unsat |= p && s < valid;
-    }
+    for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
   }
   FlOut<F, D> ob;
   fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(a, tg, cw0, w, o); });
@@ -339,10 +378,13 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 // MAXD = largest degree with a body in the switch (8 or 16): the registers of the degree-16 bodies
 // would cap every launch's occupancy, so codes with degrees <= 8 get their own instantiation.
 // 1024-thread blocks so a CU's waves share one work counter, except where the body needs more than
-// the 128 VGPRs such a block allows: the box-plus check node at MAXD=16 or in fp64 (512 threads).
-template <int WHICH, int MAXD, int KIND = 0, typename F = float>
+// the 128 VGPRs such a block allows: the box-plus check node at MAXD=16 or in fp64, and the per-pass
+// fp32 min-sum check node at MAXD=16 (512 threads). The fused kernel keeps 1024 threads (its min-sum
+// MAXD=16 body fits in 128 VGPRs; 16 waves share the phases).
+template <int WHICH, int MAXD, int KIND = 0, typename F = float, bool FUSED = false>
 constexpr int fl_block_of() {
-  return (WHICH == 0 && KIND == 1 && (MAXD > 8 || sizeof(F) == 8)) ? 512 : 1024;
+  return (WHICH == 0 && ((KIND == 1 && (MAXD > 8 || sizeof(F) == 8)) ||
+                         (!FUSED && KIND == 0 && MAXD > 8 && sizeof(F) == 4))) ? 512 : 1024;
 }
 
 // Items (node, chunk) are dealt to blocks round-robin ({b*wpb + w + nw*i}) and handed to the
@@ -465,7 +507,7 @@ __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
   }
 }
 
-// channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded
+// channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded, -0 stored as +0
 template <typename F>
 __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb) {
   const size_t total = (size_t)n * ldb;
@@ -477,7 +519,7 @@ __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int 
       const size_t k = (size_t)row * B + b;
       v = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
     }
-    dst[i] = v;
+    dst[i] = v + F(0);   // -0 -> +0 (equal values; see sign_xor)
   }
 }
 
@@ -508,6 +550,7 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
       if (p0 + r < n && b < B) {
         const size_t k = (size_t)perm[p0 + r] * B + b;
         val[it] = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
+        val[it] = val[it] + F(0);   // -0 -> +0 (equal values; see sign_xor)
       }
     }
 #pragma unroll
@@ -590,12 +633,7 @@ __device__ __forceinline__ void fused_cn_item(typename Vec<F>::T* msg, int first
   }
   if (do_par) {
 #pragma unroll
-    for (int s = 0; s < N; ++s) {
-      bool p = false;
-#pragma unroll
-      for (int j = 0; j < D; ++j) p ^= (m[j][s] < F(0));
-      unsat |= p && s < valid;
-    }
+    for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
   }
   fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
     msg[first + w * cnt + lane] = fl_pack<F>(o);
@@ -634,7 +672,7 @@ __device__ __forceinline__ void fused_vn_item(typename Vec<F>::T* msg, const typ
 }
 
 template <int KIND, typename F, int MAXD>
-__global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_fused(FlFusedArgs a) {
+__global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fused(FlFusedArgs a) {
   using V = Vec<F>;
   using VT = typename V::T;
   constexpr int N = V::N;
@@ -822,8 +860,9 @@ static const void* fl_kernel(int which, int kind, int prec, int maxd) {
              : (small ? (const void*)fl_vn<double, 8> : (const void*)fl_vn<double, 16>);
 }
 
-int fl_block(int which, int kind, int prec, int maxd) {
+int fl_block(int which, int kind, int prec, int maxd, bool fused) {
   if (which == 0 && kind == 1 && (maxd > 8 || prec == kF64)) return fl_block_of<0, 16, 1, float>();
+  if (which == 0 && !fused && kind == 0 && maxd > 8 && prec == kF32) return fl_block_of<0, 16, 0, float>();
   return fl_block_of<1, 8>();
 }
 
@@ -850,7 +889,7 @@ static const void* fl_fused_kernel(int kind, int prec, int maxd) {
 
 hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block) {
   const void* f = fl_fused_kernel(kind, prec, maxd);
-  *block = fl_block(0, kind, prec, maxd);
+  *block = fl_block(0, kind, prec, maxd, true);
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
@@ -859,7 +898,7 @@ hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blo
 hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s) {
   FlFusedArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_fused_kernel(kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd)), p, lds, s);
+  return hipLaunchKernel(fl_fused_kernel(kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd, true)), p, lds, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
