@@ -187,7 +187,7 @@ struct ibl_float {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
-  int32_t f_ncn = 0, f_nvn = 0, f_maxd = 0, f_slot16 = 0;
+  int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -788,9 +788,8 @@ int fused_setup(ibl_float* h) {
   int min_dc = 1 << 30;
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
   if (lds > (size_t)kLdsBytes || min_dc < 2 || E == 0) return IBL_OK;
-  const int maxd = std::max(g->dcm, g->dvm);
   int bpc = 0, block = 0;
-  if (fl_fused_occupancy(h->kind, h->prec, maxd, lds, &bpc, &block) != hipSuccess || bpc < 1) {
+  if (fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lds, &bpc, &block) != hipSuccess || bpc < 1) {
     (void)hipGetLastError();
     return IBL_OK;
   }
@@ -807,7 +806,6 @@ int fused_setup(ibl_float* h) {
   const std::vector<int32_t>& vn_task = ft.vn_task;
   h->f_ncn = (int32_t)(cn_task.size() / 4);
   h->f_nvn = (int32_t)(vn_task.size() / 4);
-  h->f_maxd = maxd;
   h->f_lds = lds;
   h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
@@ -1020,7 +1018,7 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   {  // same guard as the IB fast path: the float kernels are built to run without scratch
     size_t priv = 0;
     const char* kname = "";
-    HIPCHK(fl_private_bytes(kind, precision, g->dcm, g->dvm, h->fused_ok ? std::max(g->dcm, g->dvm) : 0, &priv, &kname));
+    HIPCHK(fl_private_bytes(kind, precision, g->dcm, g->dvm, h->fused_ok, &priv, &kname));
     if (priv != 0)
       return bail(fail(IBL_EHIP, std::string("float kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill): rebuild required"));
@@ -1062,7 +1060,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.ngroups = (B + cwl - 1) / cwl;
     fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
-    const size_t ntr = (size_t)34 * (2 * I + 4);
+    const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));
       HIPCHK(hipMemsetAsync(fa.trace, 0, sizeof(uint64_t) * ntr, s));
@@ -1070,7 +1068,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     const size_t esz = out_dtype == kF32 ? 4 : 8;
     fa.aligned = ((B % cwl) == 0 && ((uintptr_t)d_out % (cwl * esz)) == 0) ? 1 : 0;
     const int grid = std::min(fa.ngroups, h->f_grid);
-    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, h->f_maxd, grid, h->f_lds, s); }));
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, h->f_lds, s); }));
     if (ftrace) {
       std::vector<uint64_t> hv(ntr);
       HIPCHK(hipStreamSynchronize(s));
@@ -1086,7 +1084,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     if (early) {   // batch-global stop before imax-1: re-run the batch to L (the kernel exits if L = imax-1)
       fa.unsat = nullptr;
       fa.dL = h->dL;
-      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, h->f_maxd, grid, h->f_lds, s); }));
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, h->f_lds, s); }));
     }
     return IBL_OK;
   }

@@ -182,6 +182,10 @@ struct FlArgs {
 // in LDS for all iterations. Edge slots are numbered per check-node task (up to 64 check nodes of
 // one degree, lane = node): edge k of lane i of a task at slot first + k*count + i, so the check
 // pass reads and writes contiguous 16-byte slots; the variable pass gathers through vn_slot.
+// fused float kernel phase trace (diagnostic builds): words per phase — [0] start clock, [1 + w] wave w's
+// done clock, [17 + w] its task count, [33 + w] its first task's body start (ticket and task record
+// taken), [49 + w] that body's end
+constexpr int kFlTraceWords = 65;
 struct FlFusedArgs {
   const void* ch;           // staged channel LLRs [group][variable position] (Vec<F>::T, fl_stage_t)
   const int32_t* cn_task;   // per check task: {first slot, count, degree, 0}
@@ -269,10 +273,11 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
 // Largest private segment over the float kernels of (kind, prec, degrees); fused included when asked.
-hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, int fused_maxd, size_t* bytes,
+hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, bool fused, size_t* bytes,
                             const char** name);
-int fl_block(int which, int kind, int prec, int maxd, bool fused = false);  // threads per block of the float CN (0) / VN (1) kernels
-hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s);
-hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block);
+int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
+hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, int vmax, int grid, size_t lds,
+                           hipStream_t s);
+hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block);
 
 }  // namespace ibl

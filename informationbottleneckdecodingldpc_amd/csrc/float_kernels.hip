@@ -144,8 +144,8 @@ struct FlOut {
 // the syndrome parity of the inputs (calc_syndrome, kernels_min_and_BP.cl:206-227: parity of m < 0):
 // a check's inputs are never -0, since the staged channel holds no -0 (fl_stage*, which turn -0 into +0:
 // equal values) and a variable's output clamp(ch + sum) is -0 only if every addend is.
-template <typename F, int D>
-__device__ __forceinline__ typename Bits<F>::U sign_xor(const F (&m)[D][Vec<F>::N], int s) {
+template <typename F, int D, int NC>
+__device__ __forceinline__ typename Bits<F>::U sign_xor(const F (&m)[D][NC], int s) {
   using Bt = Bits<F>;
   typename Bt::U x = Bt::of(m[0][s]);
 #pragma unroll
@@ -155,8 +155,8 @@ __device__ __forceinline__ typename Bits<F>::U sign_xor(const F (&m)[D][Vec<F>::
 
 // Syndrome parity of codeword s's inputs: the sign bit of sign_xor (degrees <= 8); larger degrees keep
 // the compare-and-mask form (lane masks in SGPRs), which needs no VGPR beside the 16 inputs.
-template <typename F, int D>
-__device__ __forceinline__ bool syndrome_bit(const F (&m)[D][Vec<F>::N], int s) {
+template <typename F, int D, int NC>
+__device__ __forceinline__ bool syndrome_bit(const F (&m)[D][NC], int s) {
   if constexpr (D <= 8) {
     return (sign_xor<F, D>(m, s) >> (8 * sizeof(F) - 1)) != 0;
   } else {
@@ -167,10 +167,11 @@ __device__ __forceinline__ bool syndrome_bit(const F (&m)[D][Vec<F>::N], int s) 
   }
 }
 
-// Check-node body on the inputs m (min-sum or BP); put(w, o) receives output w (any order of w).
-template <int KIND, typename F, int D, class Put>
-__device__ __forceinline__ void fl_cn_body(const F (&m)[D][Vec<F>::N], F lm, Put&& put) {
-  constexpr int N = Vec<F>::N;
+// Check-node body on the inputs m of NC codewords (min-sum or BP); put(w, o) receives output w (any
+// order of w).
+template <int KIND, typename F, int D, int NC, class Put>
+__device__ __forceinline__ void fl_cn_body(const F (&m)[D][NC], F lm, Put&& put) {
+  constexpr int N = NC;
   F o[N];
   if constexpr (KIND == 0) {
     // min-sum (kernels_min_and_BP.cl:156-162): the fold t = sgn(m t) min(|t|, |m|) over the others of
@@ -304,9 +305,9 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
 }
 
 // Variable-node body on channel c and inputs m; put(w, o) receives extrinsic output w.
-template <typename F, int D, class Put>
-__device__ __forceinline__ void fl_vn_body(const F (&c)[Vec<F>::N], const F (&m)[D][Vec<F>::N], F lm, Put&& put) {
-  constexpr int N = Vec<F>::N;
+template <typename F, int D, int NC, class Put>
+__device__ __forceinline__ void fl_vn_body(const F (&c)[NC], const F (&m)[D][NC], F lm, Put&& put) {
+  constexpr int N = NC;
   F o[N];
   if constexpr (D == 1) {
 #pragma unroll
@@ -381,10 +382,19 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 // the 128 VGPRs such a block allows: the box-plus check node at MAXD=16 or in fp64, and the per-pass
 // fp32 min-sum check node at MAXD=16 (512 threads). The fused kernel keeps 1024 threads (its min-sum
 // MAXD=16 body fits in 128 VGPRs; 16 waves share the phases).
-template <int WHICH, int MAXD, int KIND = 0, typename F = float, bool FUSED = false>
+template <int WHICH, int MAXD, int KIND = 0, typename F = float>
 constexpr int fl_block_of() {
-  return (WHICH == 0 && ((KIND == 1 && (MAXD > 8 || sizeof(F) == 8)) ||
-                         (!FUSED && KIND == 0 && MAXD > 8 && sizeof(F) == 4))) ? 512 : 1024;
+  return (WHICH == 0 && ((KIND == 1 && (MAXD > 8 || sizeof(F) == 8)) || (KIND == 0 && MAXD > 8 && sizeof(F) == 4)))
+             ? 512 : 1024;
+}
+// fused kernel: 1024 threads (16 waves share the phases) unless the check bodies need more than 128 VGPRs
+// (check degree > 8, or fp64 box-plus)
+template <int CMAX, int KIND, typename F>
+constexpr int fl_fused_block_of() {
+  return (CMAX > 8 || (KIND == 1 && sizeof(F) == 8)) ? 512 : 1024;
+}
+static int fl_fused_block(int kind, int prec, int cmax) {
+  return (cmax > 8 || (kind == 1 && prec == kF64)) ? 512 : 1024;
 }
 
 // Items (node, chunk) are dealt to blocks round-robin ({b*wpb + w + nw*i}) and handed to the
@@ -611,32 +621,42 @@ __global__ void fl_send(FlArgs a) {
 // Early stop is batch-global in the reference (stop when the WHOLE batch's syndrome is zero): pass 1
 // runs imax-1 iterations and records each CN pass's syndrome in the same flag words as the per-pass
 // path; finalize_iters turns them into L; pass 2 (dL set) re-runs the batch to L only if L < imax-1.
-template <typename F>
-__device__ __forceinline__ typename Vec<F>::T fl_pack(const F (&o)[Vec<F>::N]) {
-  typename Vec<F>::T v;
+// A message slot holds Vec<F>::N codewords (16 bytes); fused tasks work on a slice of NC of them (slice h:
+// codewords h*NC .. h*NC+NC-1), read and written as NC*sizeof(F) bytes at byte offset h*NC*sizeof(F).
+template <typename F, int NC> struct Slice;
+template <> struct Slice<float, 4> { using T = float4; };
+template <> struct Slice<float, 2> { using T = float2; };
+template <> struct Slice<double, 2> { using T = double2; };
+
+template <typename F, int NC>
+__device__ __forceinline__ void slice_load(const void* base, int slot, int h, F (&v)[NC]) {
+  const typename Slice<F, NC>::T r =
+      reinterpret_cast<const typename Slice<F, NC>::T*>(base)[slot * (Vec<F>::N / NC) + h];
+  const F* e = reinterpret_cast<const F*>(&r);
 #pragma unroll
-  for (int s = 0; s < Vec<F>::N; ++s) Vec<F>::set(v, s, o[s]);
-  return v;
+  for (int s = 0; s < NC; ++s) v[s] = e[s];
+}
+template <typename F, int NC>
+__device__ __forceinline__ void slice_store(void* base, int slot, int h, const F (&v)[NC]) {
+  typename Slice<F, NC>::T r;
+  F* e = reinterpret_cast<F*>(&r);
+#pragma unroll
+  for (int s = 0; s < NC; ++s) e[s] = v[s];
+  reinterpret_cast<typename Slice<F, NC>::T*>(base)[slot * (Vec<F>::N / NC) + h] = r;
 }
 
-template <int KIND, typename F, int D>
-__device__ __forceinline__ void fused_cn_item(typename Vec<F>::T* msg, int first, int cnt, int lane, F lm,
+template <int KIND, typename F, int D, int NC>
+__device__ __forceinline__ void fused_cn_item(void* msg, int first, int cnt, int lane, int h, F lm,
                                               bool do_par, int valid, bool& unsat) {
-  using V = Vec<F>;
-  constexpr int N = V::N;
-  F m[D][N];
+  F m[D][NC];
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const typename V::T r = msg[first + j * cnt + lane];
-#pragma unroll
-    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
-  }
+  for (int j = 0; j < D; ++j) slice_load<F, NC>(msg, first + j * cnt + lane, h, m[j]);
   if (do_par) {
 #pragma unroll
-    for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
+    for (int s = 0; s < NC; ++s) unsat |= syndrome_bit<F, D>(m, s) && h * NC + s < valid;
   }
-  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
-    msg[first + w * cnt + lane] = fl_pack<F>(o);
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[NC]) __attribute__((always_inline)) {
+    slice_store<F, NC>(msg, first + w * cnt + lane, h, o);
   });
 }
 
@@ -648,37 +668,34 @@ struct SlotIdx {
   __device__ __forceinline__ int operator[](int i) const { return s16 ? (int)s16[i] : s32[i]; }
 };
 
-template <typename F, int D>
-__device__ __forceinline__ void fused_vn_item(typename Vec<F>::T* msg, const typename Vec<F>::T* chL,
-                                              const SlotIdx& vn_slot, int pos, int sfirst, int cnt, int lane, F lm) {
-  using V = Vec<F>;
-  constexpr int N = V::N;
+template <typename F, int D, int NC>
+__device__ __forceinline__ void fused_vn_item(void* msg, const void* chL, const SlotIdx& vn_slot, int pos,
+                                              int sfirst, int cnt, int lane, int h, F lm) {
   int sl[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) sl[k] = vn_slot[sfirst + k * cnt + lane];
-  F c[N], m[D][N];
-  {
-    const typename V::T r = chL[pos];
+  F c[NC], m[D][NC];
+  slice_load<F, NC>(chL, pos, h, c);
 #pragma unroll
-    for (int s = 0; s < N; ++s) c[s] = V::get(r, s);
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    const typename V::T r = msg[sl[k]];
-#pragma unroll
-    for (int s = 0; s < N; ++s) m[k][s] = V::get(r, s);
-  }
-  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { msg[sl[w]] = fl_pack<F>(o); });
+  for (int k = 0; k < D; ++k) slice_load<F, NC>(msg, sl[k], h, m[k]);
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[NC]) __attribute__((always_inline)) {
+    slice_store<F, NC>(msg, sl[w], h, o);
+  });
 }
 
-template <int KIND, typename F, int MAXD>
-__global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fused(FlFusedArgs a) {
+// CMAX / VMAX: largest check / variable degree with a body (WLAN: checks <= 8, variables up to 11 ->
+// fl_fused<.., 8, 16>, without the 16-input check bodies' registers)
+template <int KIND, typename F, int CMAX, int VMAX>
+__global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused(FlFusedArgs a) {
   using V = Vec<F>;
   using VT = typename V::T;
   constexpr int N = V::N;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   VT* msg = reinterpret_cast<VT*>(lds);
   VT* chL = msg + a.n_e;
+  // tasks take whole slots (slice 0 of N codewords): half slots (2 fp32 codewords per task, twice the
+  // tasks) measured 1.29x slower on C3 (WLAN N=1944) — the per-task latency, not the body, dominates
+  constexpr int NCs = N, h = 0;
   int* ctr = reinterpret_cast<int*>(chL + a.n_v);
   const int lane = threadIdx.x & 63;
   const F lm = (F)a.llr_max;
@@ -701,9 +718,9 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fu
 #ifndef IBL_FUSED_TRACE
 #define IBL_FUSED_TRACE 0
 #endif
-  // phase trace of block 0's first group (diagnostic builds): per phase 34 words — [0] start, [1 + w]
-  // wave w's done clock, [17 + w] its task count
+  // phase trace of block 0's first group (diagnostic builds): kFlTraceWords per phase (common.h)
   const int wv = threadIdx.x >> 6;
+  constexpr int TW = kFlTraceWords;
   uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && lane == 0) ? a.trace : nullptr;
   if (IBL_FUSED_TRACE && tr && wv == 0) tr[0] = __builtin_readcyclecounter();
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
@@ -713,19 +730,25 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fu
     for (;;) {
       const int t = take_ticket(c, lane);
       if (t >= ntasks) break;
+      if constexpr (IBL_FUSED_TRACE) {
+        if (tr && taken == 0) tr[TW * ph + 33 + wv] = __builtin_readcyclecounter();
+      }
       body(t);
+      if constexpr (IBL_FUSED_TRACE) {
+        if (tr && taken == 0) tr[TW * ph + 49 + wv] = __builtin_readcyclecounter();
+      }
       ++taken;
     }
     if constexpr (IBL_FUSED_TRACE) {
       if (tr) {
-        tr[34 * ph + 1 + wv] = __builtin_readcyclecounter();
-        tr[34 * ph + 17 + wv] = (uint64_t)taken;
+        tr[TW * ph + 1 + wv] = __builtin_readcyclecounter();
+        tr[TW * ph + 17 + wv] = (uint64_t)taken;
       }
     }
     __syncthreads();
     ++ph;
     if constexpr (IBL_FUSED_TRACE) {
-      if (tr && wv == 0) tr[34 * ph] = __builtin_readcyclecounter();
+      if (tr && wv == 0) tr[TW * ph] = __builtin_readcyclecounter();
     }
   };
   for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
@@ -749,7 +772,7 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fu
         const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
         if (lane < cnt) {
           switch (d) {
-#define X(D) case D: if constexpr (D <= MAXD) fused_cn_item<KIND, F, D>(msg, first, cnt, lane, lm, do_par, valid, unsat); break;
+#define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
             FL_DEG_CASES(X)
 #undef X
             default: break;
@@ -763,8 +786,8 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F, true>())) void fl_fu
         const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
         if (lane < cnt) {
           switch (d) {
-            case 1: fused_vn_item<F, 1>(msg, chL, vs, pos + lane, sf, cnt, lane, lm); break;
-#define X(D) case D: if constexpr (D <= MAXD) fused_vn_item<F, D>(msg, chL, vs, pos + lane, sf, cnt, lane, lm); break;
+            case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
             FL_DEG_CASES(X)
 #undef X
             default: break;
@@ -860,9 +883,9 @@ static const void* fl_kernel(int which, int kind, int prec, int maxd) {
              : (small ? (const void*)fl_vn<double, 8> : (const void*)fl_vn<double, 16>);
 }
 
-int fl_block(int which, int kind, int prec, int maxd, bool fused) {
+int fl_block(int which, int kind, int prec, int maxd) {
   if (which == 0 && kind == 1 && (maxd > 8 || prec == kF64)) return fl_block_of<0, 16, 1, float>();
-  if (which == 0 && !fused && kind == 0 && maxd > 8 && prec == kF32) return fl_block_of<0, 16, 0, float>();
+  if (which == 0 && kind == 0 && maxd > 8 && prec == kF32) return fl_block_of<0, 16, 0, float>();
   return fl_block_of<1, 8>();
 }
 
@@ -878,27 +901,30 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
   return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(fl_block(1, 0, prec, maxd)), p, 0, s);
 }
 
-static const void* fl_fused_kernel(int kind, int prec, int maxd) {
-  const bool f32 = prec == kF32, small = maxd <= 8;
-  if (kind == 0)
-    return f32 ? (small ? (const void*)fl_fused<0, float, 8> : (const void*)fl_fused<0, float, 16>)
-               : (small ? (const void*)fl_fused<0, double, 8> : (const void*)fl_fused<0, double, 16>);
-  return f32 ? (small ? (const void*)fl_fused<1, float, 8> : (const void*)fl_fused<1, float, 16>)
-             : (small ? (const void*)fl_fused<1, double, 8> : (const void*)fl_fused<1, double, 16>);
+template <int KIND, typename F>
+static const void* fl_fused_kernel_t(int cmax, int vmax) {
+  if (cmax <= 8) return vmax <= 8 ? (const void*)fl_fused<KIND, F, 8, 8> : (const void*)fl_fused<KIND, F, 8, 16>;
+  return (const void*)fl_fused<KIND, F, 16, 16>;
+}
+static const void* fl_fused_kernel(int kind, int prec, int cmax, int vmax) {
+  if (kind == 0) return prec == kF32 ? fl_fused_kernel_t<0, float>(cmax, vmax) : fl_fused_kernel_t<0, double>(cmax, vmax);
+  return prec == kF32 ? fl_fused_kernel_t<1, float>(cmax, vmax) : fl_fused_kernel_t<1, double>(cmax, vmax);
 }
 
-hipError_t fl_fused_occupancy(int kind, int prec, int maxd, size_t lds, int* blocks_per_cu, int* block) {
-  const void* f = fl_fused_kernel(kind, prec, maxd);
-  *block = fl_block(0, kind, prec, maxd, true);
+hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block) {
+  const void* f = fl_fused_kernel(kind, prec, cmax, vmax);
+  *block = fl_fused_block(kind, prec, cmax);
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
 }
 
-hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int maxd, int grid, size_t lds, hipStream_t s) {
+hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, int vmax, int grid, size_t lds,
+                           hipStream_t s) {
   FlFusedArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_fused_kernel(kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd, true)), p, lds, s);
+  return hipLaunchKernel(fl_fused_kernel(kind, prec, cmax, vmax), dim3(grid),
+                         dim3(fl_fused_block(kind, prec, cmax)), p, lds, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
@@ -907,11 +933,11 @@ hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) 
   return hipGetLastError();
 }
 
-hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, int fused_maxd, size_t* bytes,
+hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, bool fused, size_t* bytes,
                             const char** name) {
   const struct { const void* f; const char* n; } ks[] = {
       {fl_kernel(0, kind, prec, cn_maxd), "fl_cn"}, {fl_kernel(1, kind, prec, vn_maxd), "fl_vn"},
-      {fused_maxd > 0 ? fl_fused_kernel(kind, prec, fused_maxd) : nullptr, "fl_fused"}};
+      {fused ? fl_fused_kernel(kind, prec, cn_maxd, vn_maxd) : nullptr, "fl_fused"}};
   *bytes = 0;
   *name = "";
   for (const auto& k : ks) {

@@ -78,7 +78,7 @@ for s in $STEPS; do
       chk $? trace; echo "trace ok" >> $O/summary.txt;;
     ftrace)  # fused-kernel phase trace (variant `ftrace`; tools/fused_trace.py, tools/fused_trace_fl.py)
       for c in $CONFIGS; do
-        IBL_TRACE_FUSED=$O/ftrace_$c.bin IBLDPC_LIB=$VL/libibldpc_ftrace.so timeout -k 10 300 python $R/bench.py --config $c --no-cpu-baseline --steps 1 --warmup 0 > $O/ftrace_$c.json 2> $O/ftrace_$c.err
+        IBL_ALLOW_SCRATCH=1 IBL_TRACE_FUSED=$O/ftrace_$c.bin IBLDPC_LIB=$VL/libibldpc_ftrace.so timeout -k 10 300 python $R/bench.py --config $c --no-cpu-baseline --steps 1 --warmup 0 > $O/ftrace_$c.json 2> $O/ftrace_$c.err
         chk $? ftrace_$c; echo "ftrace $c ok" >> $O/summary.txt
       done;;
     mrank)   # N>1 bench path rehearsed on one GPU: 2 ranks sharing cuda:0 over gloo
