@@ -98,6 +98,16 @@ int ibl_ib_path(const ibl_ib* h);
 int ibl_ib_set_path(ibl_ib* h, int32_t path);
 int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
 /*
+ * Per-pass fast-path features (no reference counterpart; results are identical either way):
+ * IBL_FEAT_FOLD = the check pass also applies the degree-2 variables' table and writes their outputs
+ * straight into the next check inbox, and the variable pass skips those variables (codes whose checks
+ * have at most 2 degree-2 neighbours and degrees <= 8, e.g. DVB-S2's staircase, WLAN's dual diagonal).
+ * Opt-in with environment IBL_FOLD=1 at create: on MI355X the fold's check kernel runs out of registers
+ * and the decode is slower (DESIGN.md "Degree-2 fold").
+ */
+#define IBL_FEAT_FOLD 1
+int ibl_ib_features(const ibl_ib* h, int32_t* features);
+/*
  * Decode B codewords.  Replaces decode_OpenCL (discrete_LDPC_decoder_irreg.py:245-341;
  * discrete_LDPC_decoder.py:202-295).
  *   d_ch   [N][B] channel cluster ids (IBL_U8 or IBL_I32), values in [0, T_ch)

@@ -189,6 +189,7 @@ struct ItemBuf {
   int d, st, node;
   uint32_t off;            // byte offset of this lane's words in a row
   int cwb;                 // first codeword of this lane
+  int fm;                  // check pass: edge positions with a degree-2 variable (info[4*pos+3])
 };
 
 // Items of a phase: item = first + (pos - pos0) * nch + chunk (nch chunks of 512*W codewords per node)
@@ -207,6 +208,7 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.node = node;
   b.st = sload(a.info, 4 * pos + 1);
   b.d = sload(a.info, 4 * pos + 2);
+  b.fm = VN ? 0 : sload(a.info, 4 * pos + 3);
   b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * W);
   b.cwb = chunk * (512 * W) + lane * 8 * W;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
@@ -273,10 +275,36 @@ __device__ __forceinline__ void col_bases(const int8_t (&cc)[4], uint32_t lane8c
   for (int i = 0; i < 4; ++i) cb[i] = lane8c + ((uint32_t)cc[i] << 12);
 }
 
-template <int D, class Buf>
+// Degree-2 variable fold of one output word o (8 codewords): the variable's extrinsic output towards its
+// other check is table[ch][o] (vn_group<2>: one lookup per codeword in the final, matching-composed
+// degree-2 table), ch = its channel word.
+__device__ __forceinline__ uint32_t fold_word(uint32_t lane4, uint32_t ch, uint32_t o, uint32_t fbase) {
+  uint32_t t[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[k] = luc(nib(ch, k), qidx(nib(o, k), lane4), fbase);
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r |= t[k] << (4 * k);
+  return r;
+}
+
+template <int D, bool GATHER, bool FOLD, class Buf>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, const Buf& b,
                                            int fslot, bool do_par, bool& unsat) {
   constexpr int W = Buf::W;
+  // degree-2 fold (IbFastArgs::fold_mode): up to two edge positions p0 < p1 (b.fm); pass 0 gathered their
+  // channel rows as its inputs already, later passes request them here, before the node's lookups hide
+  // the latency (the fold instantiation runs 768-thread blocks: 170 VGPRs)
+  const int fm = FOLD ? b.fm : 0;
+  const int p0 = fm ? __builtin_ctz(fm) : 0;
+  const int p1 = (fm & (fm - 1)) ? __builtin_ctz(fm & (fm - 1)) : p0;
+  uint32_t fch[2][W];
+  if constexpr (FOLD && !GATHER) {
+    if (fm) {
+      load_row<W>(a.ch8 + (size_t)sload(a.fold_var, b.st + p0) * a.ldb + b.off, fch[0]);
+      load_row<W>(a.ch8 + (size_t)sload(a.fold_var, b.st + p1) * a.ldb + b.off, fch[1]);
+    }
+  }
   uint32_t outw[D][W], trow[D], cb[4];
   col_bases(a.ccol[D], lane8c, cb);
 #pragma unroll
@@ -336,8 +364,27 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 #pragma unroll
     for (int w = 0; w < D; ++w) outw[w][i] = o[w];
   }
+  if (FOLD && fm) {
+    const uint32_t ffb = slot_off(a.fold_slot);
 #pragma unroll
-  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+    for (int w = 0; w < D; ++w) {
+      if (!((fm >> w) & 1)) {
+        store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+        continue;
+      }
+      uint32_t f[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fch[0][i] : fch[1][i]);
+        f[i] = fold_word(lane4, ch, outw[w][i], ffb);
+      }
+      store_row<W>(a.fold_out + (size_t)sload(a.fold_other, b.st + w) * (uint32_t)a.ldb + b.off, f);
+      if (a.fold_mode == 2) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+  }
 }
 
 // ---------------------------------------------------------------- variable node
@@ -461,7 +508,7 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 #ifndef IBL_LIGHT_DEPTH
 #define IBL_LIGHT_DEPTH 2
 #endif
-template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2>
+template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2, bool FOLD = false>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
                                          int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat,
                                          uint64_t* trace_items, const PhaseItems pi) {
@@ -478,7 +525,7 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
       }
     } else {
       switch (cur.d) {
-#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D>(a, lane4, lane8c, cur, a.fslot[D], do_par, unsat); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D, GATHER, FOLD>(a, lane4, lane8c, cur, a.fslot[D], do_par, unsat); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
@@ -553,7 +600,7 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
   if (trace_items && lane == 0) *trace_items += (uint64_t)done;
 }
 
-template <int MAXD, bool VN, bool GATHER>
+template <int MAXD, bool VN, bool GATHER, bool FOLD = false>
 __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
@@ -585,10 +632,10 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #pragma unroll 1
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)
-      ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
+      ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD, 2, FOLD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
                                                       trace_items, PhaseItems{0, 0, a.nchunks});
     else
-      ib_phase<ItemBuf<kLightD, LW>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2)>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
+      ib_phase<ItemBuf<kLightD, LW>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2), FOLD>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
                                                    unsat, trace_items, PhaseItems{heavy_end, a.n_heavy, nch_l});
   }
   if (a.trace && lane == 0) {
@@ -611,14 +658,19 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #ifndef IBL_WPE8
 #define IBL_WPE8 1
 #endif
-template <int MAXD, bool GATHER>
-__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8 : IBL_LB16, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
+// FOLD: the degree-2 variable fold (IbFastArgs::fold_mode != 0; MAXD=8 codes only) is its own
+// instantiation, so codes without it keep the plain body's registers
+#ifndef IBL_LB8F
+#define IBL_LB8F 768
+#endif
+template <int MAXD, bool GATHER, bool FOLD = false>
+__global__ __launch_bounds__(MAXD <= 8 ? (FOLD ? IBL_LB8F : IBL_LB8) : IBL_LB16, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
   stage_pass(lds, a);
   __syncthreads();
-  ib_pass<MAXD, false, GATHER>(a, lds);
+  ib_pass<MAXD, false, GATHER, FOLD>(a, lds);
 }
 
 template <int MAXD>
@@ -1324,10 +1376,12 @@ hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch
 }
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
   if (a.gather) {
-    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, true>), dim3(grid), dim3(block), lds, s, a);
+    if (maxd <= 8 && a.fold_mode) hipLaunchKernelGGL((ib_cn_fast<8, true, true>), dim3(grid), dim3(block), lds, s, a);
+    else if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, true>), dim3(grid), dim3(block), lds, s, a);
     else hipLaunchKernelGGL((ib_cn_fast<16, true>), dim3(grid), dim3(block), lds, s, a);
   } else {
-    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, false>), dim3(grid), dim3(block), lds, s, a);
+    if (maxd <= 8 && a.fold_mode) hipLaunchKernelGGL((ib_cn_fast<8, false, true>), dim3(grid), dim3(block), lds, s, a);
+    else if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, false>), dim3(grid), dim3(block), lds, s, a);
     else hipLaunchKernelGGL((ib_cn_fast<16, false>), dim3(grid), dim3(block), lds, s, a);
   }
   return hipGetLastError();
@@ -1343,13 +1397,15 @@ hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t ld
   return hipGetLastError();
 }
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu) {
-  if (which == 0) {  // both variants must accept the LDS size; report the non-gather one
-    for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>}) {
+  if (which == 0 || which == 3) {  // every variant must accept the LDS size; report the non-gather one
+    for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>,
+                          (const void*)ib_cn_fast<8, true, true>, (const void*)ib_cn_fast<8, false, true>}) {
       hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
       if (e != hipSuccess) return e;
     }
   }
-  const void* f = which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
+  const void* f = which == 3 ? (const void*)ib_cn_fast<8, false, true>   // degree-2 fold variant (MAXD=8)
+                : which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
                 : which == 1 ? (maxd <= 8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>)
                              : (const void*)ib_dec_fast;
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
@@ -1360,16 +1416,19 @@ hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* bl
   if (block > fa.maxThreadsPerBlock) return hipErrorInvalidValue;  // above the kernel's launch bounds
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, block, lds);
 }
-hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
+hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, bool fold, size_t* bytes, const char** name) {
   const bool c8 = cn_maxd <= 8, v8 = vn_maxd <= 8;
   const struct { const void* f; const char* n; } ks[] = {
       {c8 ? (const void*)ib_cn_fast<8, true> : (const void*)ib_cn_fast<16, true>, c8 ? "ib_cn_fast<8,gather>" : "ib_cn_fast<16,gather>"},
       {c8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>, c8 ? "ib_cn_fast<8>" : "ib_cn_fast<16>"},
       {v8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>, v8 ? "ib_vn_fast<8>" : "ib_vn_fast<16>"},
-      {(const void*)ib_dec_fast, "ib_dec_fast"}};
+      {(const void*)ib_dec_fast, "ib_dec_fast"},
+      {fold ? (const void*)ib_cn_fast<8, true, true> : nullptr, "ib_cn_fast<8,gather,fold>"},
+      {fold ? (const void*)ib_cn_fast<8, false, true> : nullptr, "ib_cn_fast<8,fold>"}};
   *bytes = 0;
   *name = "";
   for (const auto& k : ks) {
+    if (!k.f) continue;
     hipFuncAttributes fa;
     const hipError_t e = hipFuncGetAttributes(&fa, k.f);
     if (e != hipSuccess) return e;

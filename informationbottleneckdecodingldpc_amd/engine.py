@@ -113,6 +113,13 @@ class IBDecoder:
         _lib.check(_lib.load().ibl_ib_path_in_use(self._h, ctypes.byref(f)), "ibl_ib_path_in_use")
         return bool(f.value)
 
+    @property
+    def fold(self) -> bool:
+        """The per-pass path folds the degree-2 variables into the check pass (``ibl_ib_features``)."""
+        f = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_ib_features(self._h, ctypes.byref(f)), "ibl_ib_features")
+        return bool(f.value & _lib.IBL_FEAT_FOLD)
+
     def decode(self, ch: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=torch.int32,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Decode ``ch`` ([N][B] cluster ids, uint8/int32, on the decoder's device)."""

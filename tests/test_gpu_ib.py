@@ -368,3 +368,25 @@ def test_misaligned_u8_channel(eng, wlan_H, path):
     dec = eng.IBDecoder(eng.Graph(g, DEV), tb, True, B, path=path)
     out = dec.decode(ch, early_stop=False).cpu().numpy()
     np.testing.assert_array_equal(out, oracle.ib_decode(g, tb, x, match=True))
+
+
+@pytest.mark.parametrize("name,imax,B,match,early", [
+    ("dvb", 8, 1100, True, False), ("dvb", 6, 700, False, True), ("wlan", 12, 2100, True, True),
+    ("wlan", 9, 300, False, False)])
+def test_ib_degree2_fold_equals_unfolded_and_oracle(eng, monkeypatch, name, imax, B, match, early, wlan_H, dvb_H):
+    """The per-pass path's degree-2 fold (the check pass applies the degree-2 variables' table and writes
+    the next check inbox; the variable pass skips them) gives the same cluster ids and stop iteration as the
+    unfolded passes (the default) and the oracle — DVB-S2's staircase and WLAN's dual-diagonal parity."""
+    g = graph.build_graph(wlan_H if name == "wlan" else dvb_H)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=imax)
+    ch = np.random.default_rng(imax + B).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    G = eng.Graph(g, DEV)
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
+    plain, it_p, dec0 = _run(eng, g, tb, ch, match, early, graph_obj=G, path="passes")
+    assert not dec0.fold                   # opt-in (IBL_FOLD=1)
+    monkeypatch.setenv("IBL_FOLD", "1")
+    folded, it_f, dec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="passes")
+    assert dec.fold
+    assert it_f == it_p == ref_it
+    np.testing.assert_array_equal(folded, ref)
+    np.testing.assert_array_equal(plain, ref)

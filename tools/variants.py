@@ -32,6 +32,8 @@ VARIANTS = {
     "lw4d2": ["IBL_LIGHT_W=4", "IBL_LIGHT_DEPTH=2"],
     # plain (cached) variable-pass row accesses instead of the default nontemporal ones
     "nt0": ["IBL_NT=0"],
+    # degree-2 fold check kernel at 1024-thread launch bounds (spills: run with IBL_ALLOW_SCRATCH=1)
+    "f1024": ["IBL_LB8F=1024"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
