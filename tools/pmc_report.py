@@ -100,7 +100,9 @@ def hbm(out, config, fetch, write, merge):
         if a:
             row.update(algorithmic_read=int(a[0]), algorithmic_write=int(a[1]),
                        fetch_over_alg=round(fa / a[0], 4), write_over_alg=round(wa / a[1], 4))
-        res[k.split("::")[-1].split("<")[0]] = row
+        key = k.split("::")[-1].split("<")[0]
+        if key not in res or row["launches"] > res[key]["launches"]:   # the loop's instantiation, not pass 0's
+            res[key] = row
         print(k, json.dumps(row))
     if merge:
         try:
