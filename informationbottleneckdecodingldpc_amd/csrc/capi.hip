@@ -183,7 +183,7 @@ struct ibl_ib {
   KTimer timer;
   // fused on-chip path (IbFusedArgs, short codes): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
-  bool fused_ok = false;
+  bool fused_ok = false, f_half_ok = false;   // f_half_ok: the 4-codeword-group kernel is usable too
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
@@ -695,7 +695,12 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     const size_t esz = out_dtype == kU8 ? 1 : 4;
     f.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
     f.ngroups = (B + 7) / 8;
-    const int grid = std::min(h->f_grid, f.ngroups);
+    // half groups (4 codewords per workgroup) when whole groups would leave workgroup slots idle;
+    // IBL_FUSED_NCW=8 / 4 forces either (A/B, tests)
+    const char* ncwe = getenv("IBL_FUSED_NCW");
+    const int ncw_env = ncwe ? atoi(ncwe) : 0;
+    f.ncw = (h->f_half_ok && (ncw_env == 4 || (ncw_env != 8 && f.ngroups < h->f_grid))) ? 4 : 8;
+    const int grid = std::min(h->f_grid, f.ngroups * (8 / f.ncw));
     // diagnostics: IBL_TRACE_FUSED=<file> records block 0's clock at every phase boundary of its first group
     const char* ftrace = getenv("IBL_TRACE_FUSED");
     const size_t ntr = (size_t)3 * (2 * I + 4);
@@ -1007,9 +1012,16 @@ int ib_fused_setup(ibl_ib* h) {
   if (dbuf) lds = lds2;
   int bpc = 0, block = 0;
   size_t priv = 0;
-  if (ib_fused_occupancy(h->CM, h->VM, lds, &bpc, &block, &priv) != hipSuccess || bpc < 1 || priv != 0) {
+  if (ib_fused_occupancy(h->CM, h->VM, 8, lds, &bpc, &block, &priv) != hipSuccess || bpc < 1 || priv != 0) {
     (void)hipGetLastError();
     return IBL_OK;
+  }
+  {   // the half-group instantiation (4 codewords per workgroup, small batches) under the same bounds
+    int bpc4 = 0, block4 = 0;
+    size_t priv4 = 0;
+    h->f_half_ok = ib_fused_occupancy(h->CM, h->VM, 4, lds, &bpc4, &block4, &priv4) == hipSuccess && bpc4 == bpc &&
+                   block4 == block && priv4 == 0;
+    (void)hipGetLastError();
   }
   FusedTasks ft;
   int rc;

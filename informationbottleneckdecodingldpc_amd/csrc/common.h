@@ -138,6 +138,7 @@ struct IbFusedArgs {
                             // (single-degree side): computed from t instead of loaded (no scalar-load
                             // wait, which also drains the wave's LDS queue, per task)
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, B, imax, half, match, out_dtype, aligned, ngroups;
+  int32_t ncw;              // codewords per workgroup: 8, or 4 (half groups, small batches; see ib_fused)
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED): block 0's clock at every phase boundary of its
                             // first group, else nullptr
 };
@@ -235,7 +236,8 @@ hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, bool fold, size_t* by
 hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT,
                              hipStream_t s);
 hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, int block, size_t lds, hipStream_t s);
-hipError_t ib_fused_occupancy(int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block, size_t* private_bytes);
+hipError_t ib_fused_occupancy(int cmax, int vmax, int ncw, size_t lds, int* blocks_per_cu, int* block,
+                              size_t* private_bytes);
 hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);

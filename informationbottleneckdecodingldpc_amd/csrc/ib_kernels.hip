@@ -118,6 +118,19 @@ template <> struct RowVec<4> { typedef uint4 T; };
 #ifndef IBL_NT
 #define IBL_NT 1
 #endif
+// Check-pass word layout. IBL_CN_STRIDED = 1: lane l's word i of a row segment is dword i*64 + l (each
+// row access of the wave is W fully coalesced 256-B dword accesses), so the check node stores word i's D
+// outputs as soon as they exist: no D x W output array stays live across the next word's lookups (-8
+// VGPRs at D = 7, W = 2). 0: lane l owns the W consecutive dwords W*l.. (one dwordxW access per row).
+// The variable pass keeps its own (contiguous) assignment: a row's byte format is the same either way.
+#ifndef IBL_CN_STRIDED
+#define IBL_CN_STRIDED 0
+#endif
+// IBL_FOLD_LATE (contiguous layout only): request the fold rows' channel words after the node's lookups
+// instead of before them (4 fewer VGPRs live across the body; the loads' latency is then exposed)
+#ifndef IBL_FOLD_LATE
+#define IBL_FOLD_LATE 0
+#endif
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 template <int W> struct RowNV;
@@ -169,6 +182,17 @@ __device__ __forceinline__ void store_row(uint8_t* p, const uint32_t (&r)[W]) {
   }
 }
 
+template <int W, bool STRIDED>
+__device__ __forceinline__ void load_words(const uint8_t* p, uint32_t (&r)[W]) {
+  if constexpr (STRIDED) {
+#pragma unroll
+    for (int i = 0; i < W; ++i) r[i] = *reinterpret_cast<const uint32_t*>(p + 256 * i);
+  } else {
+    load_row<W>(p, r);
+  }
+}
+__device__ __forceinline__ void store_word(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+
 // A wave item's inputs, fetched one item ahead of its computation (register double buffer):
 // the row loads of item k+1 are issued before item k is computed, so HBM latency overlaps the
 // lookups and the waits never cover the previous item's stores.
@@ -197,7 +221,7 @@ struct PhaseItems {
   int first, pos0, nch;
 };
 
-template <class Buf, bool VN, bool GATHER>
+template <class Buf, bool VN, bool GATHER, bool FOLD = false>
 __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, Buf& b, const PhaseItems& pi) {
   constexpr int W = Buf::W, MAXD = Buf::kMax;
   const int rel = item - pi.first;
@@ -209,15 +233,17 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.st = sload(a.info, 4 * pos + 1);
   b.d = sload(a.info, 4 * pos + 2);
   b.fm = VN ? 0 : sload(a.info, 4 * pos + 3);
-  b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * W);
-  b.cwb = chunk * (512 * W) + lane * 8 * W;
+  constexpr bool ST = !VN && IBL_CN_STRIDED;   // check-pass word layout (see cn_compute)
+  b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * (ST ? 1 : W));
+  b.cwb = chunk * (512 * W) + lane * 8 * (ST ? 1 : W);
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
+    if constexpr (ST) load_words<W, true>(row + b.off, b.row[j]);
+    else load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
   }
   if (VN) {
     load_row<W, IBL_NT>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
@@ -227,21 +253,29 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   }
   // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
   // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
-  b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
+  // fold passes (MAXD <= 8): lanes 8 + j / 16 + j carry fold_other / fold_var of edge j in the same register
+  // (vector loads: a scalar load inside the node body would wait with lgkmcnt(0), i.e. for every LDS
+  // lookup in flight)
+  if constexpr (FOLD)
+    b.tgv = (uint32_t)(lane < 8 ? a.tgt : lane < 16 ? a.fold_other : a.fold_var)[b.st + min(lane & 7, b.d - 1)];
+  else
+    b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
 }
 
 // Empty asm that consumes every register of a fetched item: the compiler inserts ONE counted
 // vmcnt wait for exactly this item's loads here (younger prefetches stay in flight), and no later
 // path (switch cases, default) leaves these registers "possibly pending" at a merge point.
-template <class Buf>
+template <bool VN, class Buf>
 __device__ __forceinline__ void settle(const Buf& b) {
   constexpr int W = Buf::W;
 #pragma unroll
   for (int j = 0; j < Buf::kMax; ++j)
 #pragma unroll
     for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.row[j][i]));
+  if constexpr (VN) {   // the check pass has no channel words (consuming constant zeros would pin 2W VGPRs)
 #pragma unroll
-  for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.chw[i]));
+    for (int i = 0; i < W; ++i) asm volatile("" ::"v"(b.chw[i]));
+  }
   asm volatile("" ::"v"(b.tgv));
 }
 
@@ -262,11 +296,12 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 #endif
 #include IBL_SCHED_FILE
 
-template <int D>
+// NCW: codewords of the word that are computed (nibbles 0 .. NCW-1; 4 = the fused kernel's half groups)
+template <int D, int NCW = 8>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
 #pragma unroll 1
-  for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
+  for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
 }
 
 // column-image addresses of the column-fetched inputs of a degree-D node (cb of colf)
@@ -288,32 +323,37 @@ __device__ __forceinline__ uint32_t fold_word(uint32_t lane4, uint32_t ch, uint3
   return r;
 }
 
+
 template <int D, bool GATHER, bool FOLD, class Buf>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, const Buf& b,
                                            int fslot, bool do_par, bool& unsat) {
   constexpr int W = Buf::W;
-  // degree-2 fold (IbFastArgs::fold_mode): up to two edge positions p0 < p1 (b.fm); pass 0 gathered their
-  // channel rows as its inputs already, later passes request them here, before the node's lookups hide
-  // the latency (the fold instantiation runs 768-thread blocks: 170 VGPRs)
+  constexpr bool ST = IBL_CN_STRIDED;
+  // degree-2 fold (IbFastArgs::fold_mode): up to two edge positions p0 < p1 (b.fm) whose variable has
+  // degree 2; their output is run through that variable's final table with its channel word and written to
+  // the variable's other check row of the next check inbox (fold_word). Pass 0 gathered those channel rows
+  // as its inputs already; later passes load them here.
   const int fm = FOLD ? b.fm : 0;
   const int p0 = fm ? __builtin_ctz(fm) : 0;
   const int p1 = (fm & (fm - 1)) ? __builtin_ctz(fm & (fm - 1)) : p0;
+  // row bases stay wave-uniform (SGPRs); the lane's byte offset is added at each access (saddr + voffset)
+  const uint8_t* fch0 = FOLD && !ST ? a.ch8 + (size_t)__builtin_amdgcn_readlane(b.tgv, 16 + p0) * a.ldb : nullptr;
+  const uint8_t* fch1 = FOLD && !ST ? a.ch8 + (size_t)__builtin_amdgcn_readlane(b.tgv, 16 + p1) * a.ldb : nullptr;
   uint32_t fch[2][W];
-  if constexpr (FOLD && !GATHER) {
-    if (fm) {
-      load_row<W>(a.ch8 + (size_t)sload(a.fold_var, b.st + p0) * a.ldb + b.off, fch[0]);
-      load_row<W>(a.ch8 + (size_t)sload(a.fold_var, b.st + p1) * a.ldb + b.off, fch[1]);
+  if constexpr (FOLD && !GATHER && !ST) {
+    if (fm && !IBL_FOLD_LATE) {
+      load_row<W>(fch0 + b.off, fch[0]);
+      load_row<W>(fch1 + b.off, fch[1]);
     }
   }
-  uint32_t outw[D][W], trow[D], cb[4];
+  uint32_t outw[ST ? 1 : D][W], trow[D], cb[4];
   col_bases(a.ccol[D], lane8c, cb);
+  if constexpr (!ST) {
 #pragma unroll
-  for (int w = 0; w < D; ++w) {
-    trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
-#pragma unroll
-    for (int i = 0; i < W; ++i) outw[w][i] = 0;
+    for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   }
   const uint32_t fbase = slot_off(fslot);
+  const uint32_t ffb = FOLD ? slot_off(a.fold_slot) : 0;
   if (do_par) {
     // Syndrome of all 8 codewords of a word at once (calc_syndrome, kernels_template_irreg.cl:
     // 304-326: parity of (m < T/2) over the check's inputs). Adding 8 - T/2 to every nibble sets
@@ -329,13 +369,25 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
       uint32_t x = (D & 1) ? 0x88888888u : 0u;
 #pragma unroll
       for (int j = 0; j < D; ++j) x ^= b.row[j][i] + bias;
-      any |= x & 0x88888888u & valid_nib8(a.B - b.cwb - 8 * i);
+      any |= x & 0x88888888u & valid_nib8(a.B - b.cwb - (ST ? 512 : 8) * i);
     }
     if (__ballot(any != 0) != 0ull) unsat = true;
   }
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    uint32_t in[D], o[D];
+    uint32_t in[D], o[D], fc[2];
+    if constexpr (FOLD && !GATHER && ST) {
+      // this word's fold channel words, requested before its lookups (row bases read out of the lanes
+      // here, so they do not occupy SGPRs across the word)
+      if (fm) {
+        uint32_t tv = b.tgv;
+        asm volatile("" : "+v"(tv));
+        const uint8_t* c0 = a.ch8 + (size_t)__builtin_amdgcn_readlane(tv, 16 + p0) * a.ldb;
+        const uint8_t* c1 = a.ch8 + (size_t)__builtin_amdgcn_readlane(tv, 16 + p1) * a.ldb;
+        fc[0] = *reinterpret_cast<const uint32_t*>(c0 + (b.off + 256u * i));
+        fc[1] = *reinterpret_cast<const uint32_t*>(c1 + (b.off + 256u * i));
+      }
+    }
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       in[j] = b.row[j][i];
@@ -361,29 +413,54 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
     } else {
       cn_word<D>(lane4, in, fbase, cb, o);
     }
+    if constexpr (ST) {
+      const uint32_t wo = b.off + 256u * i;
+      // target rows read out of the lanes at each word's stores (an opaque copy per word keeps the
+      // compiler from holding D row bases in SGPRs across the next word's lookups)
+      uint32_t tv = b.tgv;
+      asm volatile("" : "+v"(tv));
 #pragma unroll
-    for (int w = 0; w < D; ++w) outw[w][i] = o[w];
-  }
-  if (FOLD && fm) {
-    const uint32_t ffb = slot_off(a.fold_slot);
-#pragma unroll
-    for (int w = 0; w < D; ++w) {
-      if (!((fm >> w) & 1)) {
-        store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
-        continue;
+      for (int w = 0; w < D; ++w) {
+        const uint32_t tr = __builtin_amdgcn_readlane(tv, w);
+        if (FOLD && ((fm >> w) & 1)) {
+          const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fc[0] : fc[1]);
+          store_word(a.fold_out + (size_t)__builtin_amdgcn_readlane(tv, 8 + w) * (uint32_t)a.ldb + wo,
+                     fold_word(lane4, ch, o[w], ffb));
+          if (a.fold_mode == 2) store_word(a.out + (size_t)tr * (uint32_t)a.ldb + wo, o[w]);
+        } else {
+          store_word(a.out + (size_t)tr * (uint32_t)a.ldb + wo, o[w]);
+        }
       }
-      uint32_t f[W];
+    } else {
 #pragma unroll
-      for (int i = 0; i < W; ++i) {
-        const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fch[0][i] : fch[1][i]);
-        f[i] = fold_word(lane4, ch, outw[w][i], ffb);
-      }
-      store_row<W>(a.fold_out + (size_t)sload(a.fold_other, b.st + w) * (uint32_t)a.ldb + b.off, f);
-      if (a.fold_mode == 2) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+      for (int w = 0; w < D; ++w) outw[ST ? 0 : w][i] = o[w];
     }
-  } else {
+  }
+  if constexpr (!ST) {
+    if (FOLD && fm) {
+      if constexpr (!GATHER && IBL_FOLD_LATE) {
+        load_row<W>(fch0 + b.off, fch[0]);
+        load_row<W>(fch1 + b.off, fch[1]);
+      }
 #pragma unroll
-    for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+      for (int w = 0; w < D; ++w) {
+        if (!((fm >> w) & 1)) {
+          store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+          continue;
+        }
+        uint32_t f[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+          const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fch[0][i] : fch[1][i]);
+          f[i] = fold_word(lane4, ch, outw[w][i], ffb);
+        }
+        store_row<W>(a.fold_out + (size_t)__builtin_amdgcn_readlane(b.tgv, 8 + w) * (uint32_t)a.ldb + b.off, f);
+        if (a.fold_mode == 2) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+    }
   }
 }
 
@@ -392,11 +469,11 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 // c and the other inputs (kernels_template_irreg.cl:151-160): step 0 = channel table V_0,
 // step l = V_l; the last step (l = D-2) uses fslot (matching composed). Degree 1 forwards c
 // (:131-136). Schedules as for the check node (vn_group in ib_sched.inc).
-template <int D>
+template <int D, int NCW = 8>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
 #pragma unroll 1
-  for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
+  for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
 
 template <int D, class Buf>
@@ -514,7 +591,7 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
                                          uint64_t* trace_items, const PhaseItems pi) {
   // always inlined: an out-of-line body would take the item by reference through scratch
   auto compute = [&](const Buf& cur) __attribute__((always_inline)) {
-    settle(cur);
+    settle<VN>(cur);
     if constexpr (VN) {
       switch (cur.d) {
         case 1: if constexpr (DLO < 1) vn_compute<1>(a, lane4, lane8c, cur, 0); break;
@@ -549,25 +626,25 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb, Cc;
     int ia = item_of(take_ticket(ctr, lane));
     if (ia >= end) return;
-    fetch_item<Buf, VN, GATHER>(a, ia, lane, A, pi);
+    fetch_item<Buf, VN, GATHER, FOLD>(a, ia, lane, A, pi);
     int ib = item_of(take_ticket(ctr, lane));
-    fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
+    fetch_item<Buf, VN, GATHER, FOLD>(a, min(ib, end - 1), lane, Bb, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int ic = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ic, end - 1), lane, Cc, pi);
+      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ic, end - 1), lane, Cc, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (ib >= end) break;
       ia = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ia, end - 1), lane, A, pi);
+      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ia, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
       if (ic >= end) break;
       ib = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
+      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ib, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(Cc);
       ++done;
@@ -577,18 +654,18 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb;
     int item = item_of(take_ticket(ctr, lane));
     if (item >= end) return;
-    fetch_item<Buf, VN, GATHER>(a, item, lane, A, pi);
+    fetch_item<Buf, VN, GATHER, FOLD>(a, item, lane, A, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int next = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb, pi);
+      fetch_item<Buf, VN, GATHER, FOLD>(a, min(next, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (next >= end) break;
       item = next;
       next = item_of(kn);
-      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A, pi);
+      fetch_item<Buf, VN, GATHER, FOLD>(a, min(next, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
@@ -664,7 +741,18 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #define IBL_LB8F 768
 #endif
 template <int MAXD, bool GATHER, bool FOLD = false>
-__global__ __launch_bounds__(MAXD <= 8 ? (FOLD ? IBL_LB8F : IBL_LB8) : IBL_LB16, MAXD <= 8 ? IBL_WPE8 : 1) void ib_cn_fast(IbFastArgs a) {
+// check-pass bounds of their own (default: the shared ones): IBL_LB8C / IBL_WPE8C (MAXD=8), IBL_WPE8F (fold)
+#ifndef IBL_LB8C
+#define IBL_LB8C IBL_LB8
+#endif
+#ifndef IBL_WPE8C
+#define IBL_WPE8C IBL_WPE8
+#endif
+#ifndef IBL_WPE8F
+#define IBL_WPE8F IBL_WPE8
+#endif
+__global__ __launch_bounds__(MAXD <= 8 ? (FOLD ? IBL_LB8F : IBL_LB8C) : IBL_LB16,
+                             MAXD <= 8 ? (FOLD ? IBL_WPE8F : IBL_WPE8C) : 1) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
@@ -735,28 +823,28 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
 #ifndef IBL_FUSED_UNROLL
 #define IBL_FUSED_UNROLL 1
 #endif
-template <int D>
+template <int D, int NCW>
 __device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
   if constexpr (IBL_FUSED_UNROLL && D <= 6) {
 #pragma unroll
-    for (int k0 = 0; k0 < 8; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, o, k0);
+    for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, o, k0);
   } else {
-    cn_word<D>(lane4, in, fbase, cb, o);
+    cn_word<D, NCW>(lane4, in, fbase, cb, o);
   }
 }
-template <int D>
+template <int D, int NCW>
 __device__ __forceinline__ void fused_vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw, uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
   if constexpr (IBL_FUSED_UNROLL && D <= 4) {
 #pragma unroll
-    for (int k0 = 0; k0 < 8; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);
+    for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);
   } else {
-    vn_word<D>(lane4, in, chw, fbase, cb, o);
+    vn_word<D, NCW>(lane4, in, chw, fbase, cb, o);
   }
 }
 
-template <int D>
+template <int D, int NCW>
 __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt, int lane, uint32_t lane4,
                                                const IbFusedArgs& a, bool do_par, uint32_t vmask, bool& unsat) {
   uint32_t in[D], o[D];
@@ -776,7 +864,7 @@ __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt
   if constexpr (D == 2) {
     if (a.match) {
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
+      for (int g = 0; g < NCW / 4; ++g) {
         uint32_t t0[4], t1[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -792,7 +880,7 @@ __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt
     }
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};   // no column-fetched inputs (checked on the host: ncs == 0)
-    fused_cn_word<D>(lane4, in, fbase, cb, o);
+    fused_cn_word<D, NCW>(lane4, in, fbase, cb, o);
   }
 #pragma unroll
   for (int j = 0; j < D; ++j) msg[first + j * cnt + lane] = o[j];
@@ -810,7 +898,7 @@ struct VnTask {
 
 template <int MAXD>
 __device__ __forceinline__ void fetch_vn_task(const IbFusedArgs& a, const uint32_t* chg, int t, int lane,
-                                              VnTask<MAXD>& v) {
+                                              VnTask<MAXD>& v, uint32_t csh) {
   if (a.vn_uni) {
     v.pos = 64 * t;
     v.cnt = min(64, a.n_v - v.pos);
@@ -823,7 +911,7 @@ __device__ __forceinline__ void fetch_vn_task(const IbFusedArgs& a, const uint32
     v.sf = sload(a.vn_task, 4 * t + 3);
   }
   const int li = min(lane, v.cnt - 1);
-  v.chw = chg[v.pos + li];
+  v.chw = chg[v.pos + li] >> csh;   // half groups: this group's 4 codewords into nibbles 0..3
 #pragma unroll
   for (int k = 0; k < MAXD; ++k) v.sl[k] = a.vn_slot[v.sf + min(k, v.d - 1) * v.cnt + li];
 }
@@ -835,7 +923,7 @@ __device__ __forceinline__ void settle_vn(const VnTask<MAXD>& v) {
   for (int k = 0; k < MAXD; ++k) asm volatile("" ::"v"(v.sl[k]));
 }
 
-template <int D, int MAXD>
+template <int D, int MAXD, int NCW>
 __device__ __forceinline__ void fused_vn_dword(uint32_t* msg, const VnTask<MAXD>& v, uint32_t lane4,
                                                const IbFusedArgs& a) {
   uint32_t in[D], o[D];
@@ -848,21 +936,21 @@ __device__ __forceinline__ void fused_vn_dword(uint32_t* msg, const VnTask<MAXD>
     o[0] = v.chw;     // degree 1 forwards the channel value (:131-136)
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};
-    fused_vn_word<D>(lane4, in, v.chw, slot_off(a.vn_fslot[D]), cb, o);
+    fused_vn_word<D, NCW>(lane4, in, v.chw, slot_off(a.vn_fslot[D]), cb, o);
   }
 #pragma unroll
   for (int k = 0; k < D; ++k) msg[v.sl[k]] = o[k];
 }
 
 // decision of one variable for 8 codewords: fold of channel and ALL inputs, raw tables V_0..V_{D-1}
-template <int D, int MAXD>
+template <int D, int MAXD, int NCW>
 __device__ __forceinline__ void fused_dec_dword(const uint32_t* msg, const VnTask<MAXD>& v, uint32_t lane4,
                                                 uint32_t (&res)[2]) {
   uint32_t in[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) in[k] = msg[v.sl[k]];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int g = 0; g < NCW / 4; ++g) {
     uint32_t packed = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -945,8 +1033,12 @@ struct TablePrefetch {
 #define IBL_FUSED_TRACE 0
 #endif
 // CMAX / VMAX: largest check / variable degree with a body (the variable tasks' index buffers are
-// VMAX deep: a (3,6)-regular code runs ib_fused<8, 4>)
-template <int CMAX, int VMAX>
+// VMAX deep: a (3,6)-regular code runs ib_fused<8, 4>).
+// NCW: codewords per workgroup. 8 = a whole dword of nibbles per slot; 4 = half groups for small batches
+// (ceil(B/8) below the grid: C1's 1000 codewords fill 125 of 256 CUs at 8): workgroup g decodes
+// codewords 4g..4g+3 of the 8-codeword channel group g/2, held in nibbles 0..3 of its slots (the channel
+// dword shifted down; nibbles 4..7 stay unused), with half the lookups per node.
+template <int CMAX, int VMAX, int NCW = 8>
 __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(IbFusedArgs a) {
   constexpr int MAXD = VMAX;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1017,7 +1109,7 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
       }
       if (lane < cnt) {
         switch (d) {
-#define X(D) case D: if constexpr (D <= CMAX) fused_cn_dword<D>(msg, first, cnt, lane, lane4, a, do_par, vmask, unsat); break;
+#define X(D) case D: if constexpr (D <= CMAX) fused_cn_dword<D, NCW>(msg, first, cnt, lane, lane4, a, do_par, vmask, unsat); break;
           IBL_DEG_CASES(X)
 #undef X
           default: break;
@@ -1027,35 +1119,38 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   };
   // variable tasks (send / VN pass / decision): task k+1's indices and channel are fetched before task
   // k is computed (ping-pong buffers, unconditional clamped prefetch: straight-line waits)
-  auto vn_phase = [&](const uint32_t* chg, auto&& body) __attribute__((always_inline)) {
+  auto vn_phase = [&](const uint32_t* chg, uint32_t csh, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
     const int last = a.n_vn_tasks - 1;
     VnTask<MAXD> A, Bb;
     int t = take_ticket(c, lane);
     if (t > last) return;
-    fetch_vn_task(a, chg, t, lane, A);
+    fetch_vn_task(a, chg, t, lane, A, csh);
     for (;;) {
       int tn = take_ticket(c, lane);
-      fetch_vn_task(a, chg, min(tn, last), lane, Bb);
+      fetch_vn_task(a, chg, min(tn, last), lane, Bb, csh);
       settle_vn(A);
       if (lane < A.cnt) body(A);
       if (tn > last) break;
       t = take_ticket(c, lane);
-      fetch_vn_task(a, chg, min(t, last), lane, A);
+      fetch_vn_task(a, chg, min(t, last), lane, A, csh);
       settle_vn(Bb);
       if (lane < Bb.cnt) body(Bb);
       if (t > last) break;
     }
   };
-  for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+  constexpr int kSub = 8 / NCW;   // workgroup groups per channel group
+  for (int wg = blockIdx.x; wg < a.ngroups * kSub; wg += gridDim.x) {
+    const int grp = wg / kSub, sub = wg - grp * kSub;
     const uint32_t* chg = a.chT + (size_t)grp * a.n_v;   // channel by variable position (vn_node order)
-    const int cwb = grp * 8;
-    const uint32_t vmask = valid_nib8(a.B - cwb);
+    const int cwb = grp * 8 + sub * NCW;
+    const uint32_t csh = NCW == 8 ? 0u : (uint32_t)(4 * NCW * sub);
+    const uint32_t vmask = valid_nib8(a.B - cwb) & (NCW == 8 ? 0xFFFFFFFFu : 0xFFFFu);
     // send: the channel value to every edge slot of its variable
     mark(0);
     pf.load(a.cn_img, a.cn_nt);
-    vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+    vn_phase(chg, csh, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
       for (int k = 0; k < v.d; ++k) msg[a.vn_slot[v.sf + k * v.cnt + lane]] = v.chw;
     });
     next_phase();
@@ -1070,10 +1165,10 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
       next_phase();
       if (j == L) break;
       pf.load(a.cn_img + (size_t)(j + 1) * a.cn_nt * 256, a.cn_nt);
-      vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+      vn_phase(chg, csh, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
         switch (v.d) {
-          case 1: fused_vn_dword<1, MAXD>(msg, v, lane4, a); break;
-#define X(D) case D: if constexpr (D <= MAXD) fused_vn_dword<D, MAXD>(msg, v, lane4, a); break;
+          case 1: fused_vn_dword<1, MAXD, NCW>(msg, v, lane4, a); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_vn_dword<D, MAXD, NCW>(msg, v, lane4, a); break;
           IBL_DEG_CASES(X)
 #undef X
           default: break;
@@ -1082,18 +1177,18 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
       next_phase();
     }
     // decision with the tables of pass L (staged), 8 codewords of one variable per lane
-    vn_phase(chg, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
+    vn_phase(chg, csh, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
       uint32_t r[2] = {0u, 0u};
       switch (v.d) {
-        case 1: fused_dec_dword<1, MAXD>(msg, v, lane4, r); break;
-#define X(D) case D: if constexpr (D <= MAXD) fused_dec_dword<D, MAXD>(msg, v, lane4, r); break;
+        case 1: fused_dec_dword<1, MAXD, NCW>(msg, v, lane4, r); break;
+#define X(D) case D: if constexpr (D <= MAXD) fused_dec_dword<D, MAXD, NCW>(msg, v, lane4, r); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
       }
       const size_t o = (size_t)a.vn_node[v.pos + lane] * a.B + cwb;
       store4(a.out, a.out_dtype, o, 0, a.B - cwb, a.aligned != 0, r[0]);
-      store4(a.out, a.out_dtype, o, 4, a.B - cwb, a.aligned != 0, r[1]);
+      if constexpr (NCW == 8) store4(a.out, a.out_dtype, o, 4, a.B - cwb, a.aligned != 0, r[1]);
     });
     __syncthreads();   // every wave done with this group's slots before the next group's send
     mark(3 * ph + 1);
@@ -1446,7 +1541,12 @@ hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int3
   hipLaunchKernelGGL(ib_stage_t, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, perm, chT);
   return hipGetLastError();
 }
-static const void* ib_fused_kernel(int cmax, int vmax) {
+static const void* ib_fused_kernel(int cmax, int vmax, int ncw) {
+  if (ncw == 4) {
+    if (cmax <= 8 && vmax <= 4) return (const void*)ib_fused<8, 4, 4>;
+    if (cmax <= 8 && vmax <= 8) return (const void*)ib_fused<8, 8, 4>;
+    return (const void*)ib_fused<16, 16, 4>;
+  }
   if (cmax <= 8 && vmax <= 4) return (const void*)ib_fused<8, 4>;
   if (cmax <= 8 && vmax <= 8) return (const void*)ib_fused<8, 8>;
   return (const void*)ib_fused<16, 16>;
@@ -1454,10 +1554,11 @@ static const void* ib_fused_kernel(int cmax, int vmax) {
 hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, int block, size_t lds, hipStream_t s) {
   IbFusedArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(ib_fused_kernel(cmax, vmax), dim3(grid), dim3(block), p, lds, s);
+  return hipLaunchKernel(ib_fused_kernel(cmax, vmax, a.ncw), dim3(grid), dim3(block), p, lds, s);
 }
-hipError_t ib_fused_occupancy(int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block, size_t* private_bytes) {
-  const void* f = ib_fused_kernel(cmax, vmax);
+hipError_t ib_fused_occupancy(int cmax, int vmax, int ncw, size_t lds, int* blocks_per_cu, int* block,
+                              size_t* private_bytes) {
+  const void* f = ib_fused_kernel(cmax, vmax, ncw);
   // the dynamic-LDS cap is an attribute of the kernel instantiation, shared by every decoder that launches it:
   // set it to the CU's whole LDS (here and in the other *_occupancy functions), never to one decoder's size,
   // or a smaller decoder created later would lower the cap an earlier, larger one launches with

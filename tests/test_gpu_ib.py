@@ -127,9 +127,10 @@ def test_ib_mixed_degrees_fast_path(eng, match, cdegs, vdegs, fast, early):
     ("wlan", 9, 17, True, False, None),
     ("mixed16", 6, 130, False, True, None),       # every node body (degrees 2..16 / 1..16), MAXD=16
     ("mixed8", 7, 250, True, True, 4.0)])         # MAXD=8 bodies with matching, converging
-def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn0, wlan_H):
-    """The fused on-chip IB kernel (8 codewords per workgroup in LDS for all iterations) equals the
-    per-pass path and the oracle bit for bit, with the same stop iteration."""
+def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn0, wlan_H, monkeypatch):
+    """The fused on-chip IB kernel (8 codewords per workgroup in LDS for all iterations, or 4 — the
+    half groups small batches run, forced both ways with IBL_FUSED_NCW) equals the per-pass path and the
+    oracle bit for bit, with the same stop iteration."""
     H = {"reg8000": lambda: codes.regular_code(8000, 3, 6, seed=0), "wlan1944": lambda: codes.wlan_80211n(81),
          "wlan": lambda: wlan_H,
          "mixed16": lambda: _mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15),
@@ -144,15 +145,18 @@ def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn
         tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
         ch = q.sample_all_zero(g.n_v, B, np.random.default_rng(B)).astype(np.int32)
     ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
-    fo, fit, fdec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="fused", out_dtype=torch.uint8,
-                         ch_dtype=torch.uint8)
-    assert fdec.fused
+    for ncw in ("8", "4"):
+        monkeypatch.setenv("IBL_FUSED_NCW", ncw)
+        fo, fit, fdec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="fused", out_dtype=torch.uint8,
+                             ch_dtype=torch.uint8)
+        assert fdec.fused
+        assert fit == ref_it, ncw
+        np.testing.assert_array_equal(fo, ref, err_msg=f"IBL_FUSED_NCW={ncw}")
     po, pit, pdec = _run(eng, g, tb, ch, match, early, graph_obj=G, path="passes")
     assert not pdec.fused
-    assert fit == pit == ref_it
+    assert pit == ref_it
     if name == "reg8000" and early:
         assert ref_it < imax - 1
-    np.testing.assert_array_equal(fo, ref)
     np.testing.assert_array_equal(po, ref)
 
 
@@ -161,7 +165,8 @@ def test_ib_fused_table_sets(eng, name, wlan_H, monkeypatch):
     """Both table-staging modes of the fused kernel (two LDS table sets where they fit, as for the
     (3,6) N=8000 code; one set + raw buffer otherwise, forced with IBL_FUSED_DBUF=0) equal the oracle;
     B = 4100 gives 513 groups of 8 codewords (a ragged last one), so workgroups run 2-3 groups and the
-    set parity carries across the group boundary."""
+    set parity carries across the group boundary (also with 4-codeword half groups: 1025 workgroup
+    groups)."""
     H = codes.regular_code(8000, 3, 6, seed=0) if name == "reg8000" else wlan_H
     g = graph.build_graph(H)
     G = eng.Graph(g, DEV)
@@ -169,14 +174,13 @@ def test_ib_fused_table_sets(eng, name, wlan_H, monkeypatch):
     tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 11)
     ch = q.sample_all_zero(g.n_v, 4100, np.random.default_rng(4)).astype(np.int32)
     ref = oracle.ib_decode(g, tb, ch, match=True, early_stop=False)
-    outs = []
     for mode in ("1", "0"):
-        monkeypatch.setenv("IBL_FUSED_DBUF", mode)
-        fo, _, fdec = _run(eng, g, tb, ch, True, False, graph_obj=G, path="fused")
-        assert fdec.fused
-        outs.append(fo)
-    np.testing.assert_array_equal(outs[0], ref)
-    np.testing.assert_array_equal(outs[1], ref)
+        for ncw in ("8", "4"):
+            monkeypatch.setenv("IBL_FUSED_DBUF", mode)
+            monkeypatch.setenv("IBL_FUSED_NCW", ncw)
+            fo, _, fdec = _run(eng, g, tb, ch, True, False, graph_obj=G, path="fused")
+            assert fdec.fused
+            np.testing.assert_array_equal(fo, ref, err_msg=f"IBL_FUSED_DBUF={mode} IBL_FUSED_NCW={ncw}")
 
 
 def test_ib_fused_path_selection(eng, wlan_H, dvb_H):

@@ -34,6 +34,17 @@ VARIANTS = {
     "nt0": ["IBL_NT=0"],
     # degree-2 fold check kernel at 1024-thread launch bounds (spills: run with IBL_ALLOW_SCRATCH=1)
     "f1024": ["IBL_LB8F=1024"],
+    # check-pass strided word layout (lane l's word i = dword 64 i + l; outputs stored per word), and the
+    # same with the fold kernel at 1024-thread launch bounds
+    "cst": ["IBL_CN_STRIDED=1"],
+    "cstf": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024"],
+    # check schedule of 2 codewords x 4 chains (half the column-term registers of 4 x 2): alone, with the
+    # strided layout, with the fold kernel at 1024 threads, and with 5 check waves per SIMD (256-thread blocks)
+    "s2n": ['IBL_SCHED_FILE="ib_sched_s2n.inc"'],
+    "cs2": ["IBL_CN_STRIDED=1", 'IBL_SCHED_FILE="ib_sched_cs2.inc"'],
+    "cs2f": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024", 'IBL_SCHED_FILE="ib_sched_cs2f.inc"'],
+    "cs2o5": ["IBL_CN_STRIDED=1", "IBL_LB8C=256", "IBL_WPE8C=5", "IBL_LB8F=1024",
+              'IBL_SCHED_FILE="ib_sched_cs2o5.inc"'],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
@@ -45,7 +56,8 @@ VARIANTS = {
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
 }
 # gen_sched.py arguments of the variants that need their own schedule file
-SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3"}
+SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3",
+              "s2n": "2 4 2 4 0 0", "cs2": "2 4 2 4 0 0", "cs2f": "2 4 2 4 0 0", "cs2o5": "2 4 2 4 0 0"}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
