@@ -72,16 +72,6 @@ __device__ __forceinline__ int take_ticket(int* ctr, int lane) {
   return __builtin_amdgcn_readfirstlane(t);
 }
 
-// The same ticket in two halves: the LDS atomic is issued now and read back (readfirstlane) later, after
-// other LDS work of the wave — the read-back then waits only for the atomic, whereas taking a ticket
-// right after a task's slot stores waits for those stores too (LDS returns in order).
-__device__ __forceinline__ int ticket_issue(int* ctr, int lane) {
-  int t = 0;
-  if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return t;
-}
-__device__ __forceinline__ int ticket_read(int t) { return __builtin_amdgcn_readfirstlane(t); }
-
 // ---------------------------------------------------------------- IB fast path
 struct IbFastArgs {
   const uint8_t* in;        // own-order inbox (nullptr for CN pass 0: inputs gathered from ch8)

@@ -723,25 +723,13 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   constexpr int TW = kFlTraceWords;
   uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && lane == 0) ? a.trace : nullptr;
   if (IBL_FUSED_TRACE && tr && wv == 0) tr[0] = __builtin_readcyclecounter();
-#ifndef IBL_TICKET_AHEAD
-#define IBL_TICKET_AHEAD 0
-#endif
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
     int taken = 0;
-#if IBL_TICKET_AHEAD
-    int tv = ticket_issue(c, lane);
-#endif
     for (;;) {
-#if IBL_TICKET_AHEAD
-      const int t = ticket_read(tv);
-      if (t >= ntasks) break;
-      tv = ticket_issue(c, lane);   // the next task's ticket, read after this task's LDS work
-#else
       const int t = take_ticket(c, lane);
       if (t >= ntasks) break;
-#endif
       if constexpr (IBL_FUSED_TRACE) {
         if (tr && taken == 0) tr[TW * ph + 33 + wv] = __builtin_readcyclecounter();
       }

@@ -1032,14 +1032,6 @@ struct TablePrefetch {
 #ifndef IBL_FUSED_TRACE
 #define IBL_FUSED_TRACE 0
 #endif
-// fused kernels: the next task's ticket is issued before the current task's LDS work (ticket_issue)
-#ifndef IBL_TICKET_AHEAD
-#define IBL_TICKET_AHEAD 0
-#endif
-// variable tasks in flight per wave in the fused kernel's variable-type phases (2 = ping-pong, 3)
-#ifndef IBL_FUSED_VDEPTH
-#define IBL_FUSED_VDEPTH 2
-#endif
 // CMAX / VMAX: largest check / variable degree with a body (the variable tasks' index buffers are
 // VMAX deep: a (3,6)-regular code runs ib_fused<8, 4>).
 // NCW: codewords per workgroup. 8 = a whole dword of nibbles per slot; 4 = half groups for small batches
@@ -1102,18 +1094,9 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   auto cn_phase = [&](bool do_par, uint32_t vmask, bool& unsat) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
-#if IBL_TICKET_AHEAD
-    int tv = ticket_issue(c, lane);
-#endif
     for (;;) {
-#if IBL_TICKET_AHEAD
-      const int t = ticket_read(tv);
-      if (t >= a.n_cn_tasks) break;
-      tv = ticket_issue(c, lane);   // the next task's ticket, read after this task's LDS work
-#else
       const int t = take_ticket(c, lane);
       if (t >= a.n_cn_tasks) break;
-#endif
       int first, cnt, d;
       if (a.cn_uni) {
         d = a.cn_uni;
@@ -1140,53 +1123,10 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
     const int last = a.n_vn_tasks - 1;
-#if IBL_FUSED_VDEPTH == 3
-    // three tasks in flight: task k+2's slot indices and channel are requested before task k is computed
-    VnTask<MAXD> A, Bb, Cc;
-    int ta = take_ticket(c, lane);
-    if (ta > last) return;
-    fetch_vn_task(a, chg, ta, lane, A, csh);
-    int tb = take_ticket(c, lane);
-    fetch_vn_task(a, chg, min(tb, last), lane, Bb, csh);
-    for (;;) {
-      const int tc = take_ticket(c, lane);
-      fetch_vn_task(a, chg, min(tc, last), lane, Cc, csh);
-      settle_vn(A);
-      if (lane < A.cnt) body(A);
-      if (tb > last) break;
-      ta = take_ticket(c, lane);
-      fetch_vn_task(a, chg, min(ta, last), lane, A, csh);
-      settle_vn(Bb);
-      if (lane < Bb.cnt) body(Bb);
-      if (tc > last) break;
-      tb = take_ticket(c, lane);
-      fetch_vn_task(a, chg, min(tb, last), lane, Bb, csh);
-      settle_vn(Cc);
-      if (lane < Cc.cnt) body(Cc);
-      if (ta > last) break;
-    }
-#else
     VnTask<MAXD> A, Bb;
     int t = take_ticket(c, lane);
     if (t > last) return;
     fetch_vn_task(a, chg, t, lane, A, csh);
-#if IBL_TICKET_AHEAD
-    int tv = ticket_issue(c, lane);
-    for (;;) {
-      int tn = ticket_read(tv);
-      fetch_vn_task(a, chg, min(tn, last), lane, Bb, csh);
-      tv = ticket_issue(c, lane);
-      settle_vn(A);
-      if (lane < A.cnt) body(A);
-      if (tn > last) break;
-      t = ticket_read(tv);
-      fetch_vn_task(a, chg, min(t, last), lane, A, csh);
-      tv = ticket_issue(c, lane);
-      settle_vn(Bb);
-      if (lane < Bb.cnt) body(Bb);
-      if (t > last) break;
-    }
-#else
     for (;;) {
       int tn = take_ticket(c, lane);
       fetch_vn_task(a, chg, min(tn, last), lane, Bb, csh);
@@ -1199,8 +1139,6 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
       if (lane < Bb.cnt) body(Bb);
       if (t > last) break;
     }
-#endif
-#endif
   };
   constexpr int kSub = 8 / NCW;   // workgroup groups per channel group
   for (int wg = blockIdx.x; wg < a.ngroups * kSub; wg += gridDim.x) {

@@ -45,11 +45,6 @@ VARIANTS = {
     "cs2f": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024", 'IBL_SCHED_FILE="ib_sched_cs2f.inc"'],
     "cs2o5": ["IBL_CN_STRIDED=1", "IBL_LB8C=256", "IBL_WPE8C=5", "IBL_LB8F=1024",
               'IBL_SCHED_FILE="ib_sched_cs2o5.inc"'],
-    # fused kernels (IB and float): the next task's ticket issued before the current task's LDS work
-    "tka": ["IBL_TICKET_AHEAD=1"],
-    "tka3": ["IBL_TICKET_AHEAD=1", "IBL_FUSED_VDEPTH=3"],
-    # fused IB kernel: three variable tasks in flight per wave
-    "fvd3": ["IBL_FUSED_VDEPTH=3"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
