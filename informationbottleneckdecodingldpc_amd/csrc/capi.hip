@@ -917,7 +917,7 @@ int fused_setup(ibl_float* h) {
     size_t priv = 0;
     if (lc <= (size_t)kLdsBytes / 2 &&
         fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lc, &bpc_c, &block_c, true, &priv) == hipSuccess &&
-        bpc_c >= 2 && (priv == 0 || getenv("IBL_ALLOW_SCRATCH"))) {
+        bpc_c >= 2 && priv == 0) {
       h->f_compact_ok = true;
       h->f_lds_c = lc;
       h->f_slot16_c = s16c ? 1 : 0;

@@ -690,12 +690,8 @@ __device__ __forceinline__ void fused_vn_item(void* msg, const void* chL, const 
 // 8-byte slots, half the LDS, so two 512-thread workgroups share a CU and each one's phase boundaries
 // (barrier waits, the tiered ends of its waves' tasks) overlap the other's work. The staged channel stays
 // in 4-codeword groups (fl_stage_t); compact group g reads half g & 1 of channel group g >> 1.
-#ifndef IBL_FUSED_CBLK
-#define IBL_FUSED_CBLK 512   // threads per compact workgroup (two per CU)
-#endif
 template <int KIND, typename F, int CMAX, int VMAX, int G = Vec<F>::N>
-__global__ __launch_bounds__((G < Vec<F>::N ? IBL_FUSED_CBLK : fl_fused_block_of<CMAX, KIND, F>()),
-                             (G < Vec<F>::N ? IBL_FUSED_CBLK / 128 : 1))
+__global__ __launch_bounds__((G < Vec<F>::N ? 512 : fl_fused_block_of<CMAX, KIND, F>()), (G < Vec<F>::N ? 4 : 1))
 void fl_fused(FlFusedArgs a) {
   using VT = typename Slice<F, G>::T;
   constexpr int N = G;
@@ -931,7 +927,7 @@ static const void* fl_fused_kernel(int kind, int prec, int cmax, int vmax, bool 
 hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block,
                               bool compact, size_t* private_bytes) {
   const void* f = fl_fused_kernel(kind, prec, cmax, vmax, compact);
-  *block = compact ? IBL_FUSED_CBLK : fl_fused_block(kind, prec, cmax);
+  *block = compact ? 512 : fl_fused_block(kind, prec, cmax);
   if (private_bytes) {
     hipFuncAttributes fa;
     hipError_t e = hipFuncGetAttributes(&fa, f);
@@ -948,7 +944,7 @@ hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, i
   FlFusedArgs args = a;
   void* p[] = {&args};
   return hipLaunchKernel(fl_fused_kernel(kind, prec, cmax, vmax, compact), dim3(grid),
-                         dim3(compact ? IBL_FUSED_CBLK : fl_fused_block(kind, prec, cmax)), p, lds, s);
+                         dim3(compact ? 512 : fl_fused_block(kind, prec, cmax)), p, lds, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {

@@ -45,8 +45,6 @@ VARIANTS = {
     "cs2f": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024", 'IBL_SCHED_FILE="ib_sched_cs2f.inc"'],
     "cs2o5": ["IBL_CN_STRIDED=1", "IBL_LB8C=256", "IBL_WPE8C=5", "IBL_LB8F=1024",
               'IBL_SCHED_FILE="ib_sched_cs2o5.inc"'],
-    # compact fused float groups in 1024-thread workgroups (two per CU: 8 waves per SIMD)
-    "fcb1024": ["IBL_FUSED_CBLK=1024"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
