@@ -208,11 +208,6 @@ struct ibl_float {
   int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
   size_t f_lds = 0;
   int f_grid = 0;
-  // compact fp32 groups (2 codewords, 8-byte slots, two 512-thread workgroups per CU): usable / chosen
-  bool f_compact_ok = false, f_compact = false;
-  int32_t f_slot16_c = 0;
-  size_t f_lds_c = 0;
-  int f_grid_c = 0;
 };
 
 extern "C" {
@@ -906,27 +901,6 @@ int fused_setup(ibl_float* h) {
   h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
   h->fused_ok = true;
-  // compact fp32 groups: (E + N) 8-byte slots per workgroup, the u16 slot indices only if two workgroups
-  // still fit a CU; IBL_FUSED_FCW=2 / 4 forces compact / 4-codeword groups
-  if (h->prec == kF32) {
-    size_t lc = (size_t)(E + g->n_v) * 8 + 16;
-    const size_t lc16 = lc + (size_t)E * 2;
-    const bool s16c = E < 65536 && lc16 <= (size_t)kLdsBytes / 2 && !(s16e && s16e[0] == '0');
-    if (s16c) lc = lc16;
-    int bpc_c = 0, block_c = 0;
-    size_t priv = 0;
-    if (lc <= (size_t)kLdsBytes / 2 &&
-        fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lc, &bpc_c, &block_c, true, &priv) == hipSuccess &&
-        bpc_c >= 2 && priv == 0) {
-      h->f_compact_ok = true;
-      h->f_lds_c = lc;
-      h->f_slot16_c = s16c ? 1 : 0;
-      h->f_grid_c = bpc_c * g->num_cus;
-    }
-    (void)hipGetLastError();
-    const char* fcw = getenv("IBL_FUSED_FCW");
-    h->f_compact = h->f_compact_ok && fcw && atoi(fcw) == 2;
-  }
   return IBL_OK;
 }
 
@@ -1181,11 +1155,8 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
     fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
     fa.n_vn_tasks = h->f_nvn; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
-    const bool compact = h->f_compact;
-    const int cwg = compact ? 2 : cwl;    // codewords per workgroup group
-    fa.ngroups = (B + cwg - 1) / cwg;
-    fa.slot16 = compact ? h->f_slot16_c : h->f_slot16;
-    const size_t flds = compact ? h->f_lds_c : h->f_lds;
+    fa.ngroups = (B + cwl - 1) / cwl;
+    fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
     const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {
@@ -1193,9 +1164,9 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
       HIPCHK(hipMemsetAsync(fa.trace, 0, sizeof(uint64_t) * ntr, s));
     }
     const size_t esz = out_dtype == kF32 ? 4 : 8;
-    fa.aligned = ((B % cwg) == 0 && ((uintptr_t)d_out % (cwg * esz)) == 0) ? 1 : 0;
-    const int grid = std::min(fa.ngroups, compact ? h->f_grid_c : h->f_grid);
-    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, flds, s, compact); }));
+    fa.aligned = ((B % cwl) == 0 && ((uintptr_t)d_out % (cwl * esz)) == 0) ? 1 : 0;
+    const int grid = std::min(fa.ngroups, h->f_grid);
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, h->f_lds, s); }));
     if (ftrace) {
       std::vector<uint64_t> hv(ntr);
       HIPCHK(hipStreamSynchronize(s));
@@ -1211,7 +1182,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     if (early) {   // batch-global stop before imax-1: re-run the batch to L (the kernel exits if L = imax-1)
       fa.unsat = nullptr;
       fa.dL = h->dL;
-      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, flds, s, compact); }));
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, h->f_lds, s); }));
     }
     return IBL_OK;
   }

@@ -287,8 +287,7 @@ hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, bool f
                             const char** name);
 int fl_block(int which, int kind, int prec, int maxd);  // threads per block of the float CN (0) / VN (1) kernels
 hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, int vmax, int grid, size_t lds,
-                           hipStream_t s, bool compact = false);
-hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block,
-                              bool compact = false, size_t* private_bytes = nullptr);
+                           hipStream_t s);
+hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block);
 
 }  // namespace ibl

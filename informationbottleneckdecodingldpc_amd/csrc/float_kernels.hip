@@ -628,36 +628,35 @@ template <> struct Slice<float, 4> { using T = float4; };
 template <> struct Slice<float, 2> { using T = float2; };
 template <> struct Slice<double, 2> { using T = double2; };
 
-// SL = slices per slot: Vec<F>::N / NC for 16-byte slots, 1 when the slots themselves hold NC codewords
-// (the compact 2-codeword fp32 groups, 8-byte slots)
-template <typename F, int NC, int SL = Vec<F>::N / NC>
+template <typename F, int NC>
 __device__ __forceinline__ void slice_load(const void* base, int slot, int h, F (&v)[NC]) {
-  const typename Slice<F, NC>::T r = reinterpret_cast<const typename Slice<F, NC>::T*>(base)[slot * SL + h];
+  const typename Slice<F, NC>::T r =
+      reinterpret_cast<const typename Slice<F, NC>::T*>(base)[slot * (Vec<F>::N / NC) + h];
   const F* e = reinterpret_cast<const F*>(&r);
 #pragma unroll
   for (int s = 0; s < NC; ++s) v[s] = e[s];
 }
-template <typename F, int NC, int SL = Vec<F>::N / NC>
+template <typename F, int NC>
 __device__ __forceinline__ void slice_store(void* base, int slot, int h, const F (&v)[NC]) {
   typename Slice<F, NC>::T r;
   F* e = reinterpret_cast<F*>(&r);
 #pragma unroll
   for (int s = 0; s < NC; ++s) e[s] = v[s];
-  reinterpret_cast<typename Slice<F, NC>::T*>(base)[slot * SL + h] = r;
+  reinterpret_cast<typename Slice<F, NC>::T*>(base)[slot * (Vec<F>::N / NC) + h] = r;
 }
 
-template <int KIND, typename F, int D, int NC, int SL = Vec<F>::N / NC>
+template <int KIND, typename F, int D, int NC>
 __device__ __forceinline__ void fused_cn_item(void* msg, int first, int cnt, int lane, int h, F lm,
                                               bool do_par, int valid, bool& unsat) {
   F m[D][NC];
 #pragma unroll
-  for (int j = 0; j < D; ++j) slice_load<F, NC, SL>(msg, first + j * cnt + lane, h, m[j]);
+  for (int j = 0; j < D; ++j) slice_load<F, NC>(msg, first + j * cnt + lane, h, m[j]);
   if (do_par) {
 #pragma unroll
     for (int s = 0; s < NC; ++s) unsat |= syndrome_bit<F, D>(m, s) && h * NC + s < valid;
   }
   fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[NC]) __attribute__((always_inline)) {
-    slice_store<F, NC, SL>(msg, first + w * cnt + lane, h, o);
+    slice_store<F, NC>(msg, first + w * cnt + lane, h, o);
   });
 }
 
@@ -669,39 +668,34 @@ struct SlotIdx {
   __device__ __forceinline__ int operator[](int i) const { return s16 ? (int)s16[i] : s32[i]; }
 };
 
-template <typename F, int D, int NC, int SL = Vec<F>::N / NC>
+template <typename F, int D, int NC>
 __device__ __forceinline__ void fused_vn_item(void* msg, const void* chL, const SlotIdx& vn_slot, int pos,
                                               int sfirst, int cnt, int lane, int h, F lm) {
   int sl[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) sl[k] = vn_slot[sfirst + k * cnt + lane];
   F c[NC], m[D][NC];
-  slice_load<F, NC, SL>(chL, pos, h, c);
+  slice_load<F, NC>(chL, pos, h, c);
 #pragma unroll
-  for (int k = 0; k < D; ++k) slice_load<F, NC, SL>(msg, sl[k], h, m[k]);
+  for (int k = 0; k < D; ++k) slice_load<F, NC>(msg, sl[k], h, m[k]);
   fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[NC]) __attribute__((always_inline)) {
-    slice_store<F, NC, SL>(msg, sl[w], h, o);
+    slice_store<F, NC>(msg, sl[w], h, o);
   });
 }
 
 // CMAX / VMAX: largest check / variable degree with a body (WLAN: checks <= 8, variables up to 11 ->
 // fl_fused<.., 8, 16>, without the 16-input check bodies' registers)
-// G: codewords per workgroup group. G = Vec<F>::N: 16-byte slots; G = 2 with fp32 ("compact" groups):
-// 8-byte slots, half the LDS, so two 512-thread workgroups share a CU and each one's phase boundaries
-// (barrier waits, the tiered ends of its waves' tasks) overlap the other's work. The staged channel stays
-// in 4-codeword groups (fl_stage_t); compact group g reads half g & 1 of channel group g >> 1.
-template <int KIND, typename F, int CMAX, int VMAX, int G = Vec<F>::N>
-__global__ __launch_bounds__((G < Vec<F>::N ? 512 : fl_fused_block_of<CMAX, KIND, F>()), (G < Vec<F>::N ? 4 : 1))
-void fl_fused(FlFusedArgs a) {
-  using VT = typename Slice<F, G>::T;
-  constexpr int N = G;
-  constexpr int CH_SL = Vec<F>::N / G;   // channel slices per staged channel slot
+template <int KIND, typename F, int CMAX, int VMAX>
+__global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused(FlFusedArgs a) {
+  using V = Vec<F>;
+  using VT = typename V::T;
+  constexpr int N = V::N;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   VT* msg = reinterpret_cast<VT*>(lds);
   VT* chL = msg + a.n_e;
-  // tasks take whole slots: half slots of a 16-byte slot (2 fp32 codewords per task, twice the tasks, one
-  // workgroup) measured 1.29x slower on C3 (WLAN N=1944) — the per-task latency, not the body, dominates
-  constexpr int NCs = N, h = 0, SL = 1;
+  // tasks take whole slots (slice 0 of N codewords): half slots (2 fp32 codewords per task, twice the
+  // tasks) measured 1.29x slower on C3 (WLAN N=1944) — the per-task latency, not the body, dominates
+  constexpr int NCs = N, h = 0;
   int* ctr = reinterpret_cast<int*>(chL + a.n_v);
   const int lane = threadIdx.x & 63;
   const F lm = (F)a.llr_max;
@@ -766,7 +760,7 @@ void fl_fused(FlFusedArgs a) {
       const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
       if (lane < cnt) {
         // channel staged as [group][variable position] (fl_stage_t): a task reads consecutive slots
-        const VT c = reinterpret_cast<const VT*>(a.ch)[((size_t)(grp / CH_SL) * a.n_v + pos + lane) * CH_SL + grp % CH_SL];
+        const VT c = reinterpret_cast<const VT*>(a.ch)[(size_t)grp * a.n_v + pos + lane];
         chL[pos + lane] = c;
         for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
       }
@@ -778,7 +772,7 @@ void fl_fused(FlFusedArgs a) {
         const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
         if (lane < cnt) {
           switch (d) {
-#define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs, SL>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
+#define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
             FL_DEG_CASES(X)
 #undef X
             default: break;
@@ -792,8 +786,8 @@ void fl_fused(FlFusedArgs a) {
         const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
         if (lane < cnt) {
           switch (d) {
-            case 1: fused_vn_item<F, 1, NCs, SL>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
-#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs, SL>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+            case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
             FL_DEG_CASES(X)
 #undef X
             default: break;
@@ -811,13 +805,13 @@ void fl_fused(FlFusedArgs a) {
         {
           const VT r = chL[pos + lane];
 #pragma unroll
-          for (int s = 0; s < N; ++s) x[s] = reinterpret_cast<const F*>(&r)[s];
+          for (int s = 0; s < N; ++s) x[s] = V::get(r, s);
         }
         if (L > 0)
           for (int k = 0; k < d; ++k) {
             const VT r = msg[vs[sf + k * cnt + lane]];
 #pragma unroll
-            for (int s = 0; s < N; ++s) x[s] = x[s] + reinterpret_cast<const F*>(&r)[s];
+            for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
           }
         const size_t o = (size_t)node * a.B + cw0;
         if (a.out_dtype == kF32) {
@@ -825,11 +819,6 @@ void fl_fused(FlFusedArgs a) {
           if constexpr (N == 4) {
             if (a.aligned && valid >= 4) {
               *reinterpret_cast<float4*>(p) = make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
-              return;
-            }
-          } else if constexpr (N == 2) {
-            if (a.aligned && valid >= 2) {
-              *reinterpret_cast<float2*>(p) = make_float2((float)x[0], (float)x[1]);
               return;
             }
           }
@@ -912,39 +901,30 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
   return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(fl_block(1, 0, prec, maxd)), p, 0, s);
 }
 
-template <int KIND, typename F, int G = Vec<F>::N>
+template <int KIND, typename F>
 static const void* fl_fused_kernel_t(int cmax, int vmax) {
-  if (cmax <= 8) return vmax <= 8 ? (const void*)fl_fused<KIND, F, 8, 8, G> : (const void*)fl_fused<KIND, F, 8, 16, G>;
-  return (const void*)fl_fused<KIND, F, 16, 16, G>;
+  if (cmax <= 8) return vmax <= 8 ? (const void*)fl_fused<KIND, F, 8, 8> : (const void*)fl_fused<KIND, F, 8, 16>;
+  return (const void*)fl_fused<KIND, F, 16, 16>;
 }
-// compact: 2-codeword fp32 groups (8-byte slots, 512-thread workgroups, two per CU)
-static const void* fl_fused_kernel(int kind, int prec, int cmax, int vmax, bool compact) {
-  if (compact) return kind == 0 ? fl_fused_kernel_t<0, float, 2>(cmax, vmax) : fl_fused_kernel_t<1, float, 2>(cmax, vmax);
+static const void* fl_fused_kernel(int kind, int prec, int cmax, int vmax) {
   if (kind == 0) return prec == kF32 ? fl_fused_kernel_t<0, float>(cmax, vmax) : fl_fused_kernel_t<0, double>(cmax, vmax);
   return prec == kF32 ? fl_fused_kernel_t<1, float>(cmax, vmax) : fl_fused_kernel_t<1, double>(cmax, vmax);
 }
 
-hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block,
-                              bool compact, size_t* private_bytes) {
-  const void* f = fl_fused_kernel(kind, prec, cmax, vmax, compact);
-  *block = compact ? 512 : fl_fused_block(kind, prec, cmax);
-  if (private_bytes) {
-    hipFuncAttributes fa;
-    hipError_t e = hipFuncGetAttributes(&fa, f);
-    if (e != hipSuccess) return e;
-    *private_bytes = fa.localSizeBytes;
-  }
+hipError_t fl_fused_occupancy(int kind, int prec, int cmax, int vmax, size_t lds, int* blocks_per_cu, int* block) {
+  const void* f = fl_fused_kernel(kind, prec, cmax, vmax);
+  *block = fl_fused_block(kind, prec, cmax);
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
   if (e != hipSuccess) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, *block, lds);
 }
 
 hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, int vmax, int grid, size_t lds,
-                           hipStream_t s, bool compact) {
+                           hipStream_t s) {
   FlFusedArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_fused_kernel(kind, prec, cmax, vmax, compact), dim3(grid),
-                         dim3(compact ? 512 : fl_fused_block(kind, prec, cmax)), p, lds, s);
+  return hipLaunchKernel(fl_fused_kernel(kind, prec, cmax, vmax), dim3(grid),
+                         dim3(fl_fused_block(kind, prec, cmax)), p, lds, s);
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
@@ -957,7 +937,7 @@ hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, bool f
                             const char** name) {
   const struct { const void* f; const char* n; } ks[] = {
       {fl_kernel(0, kind, prec, cn_maxd), "fl_cn"}, {fl_kernel(1, kind, prec, vn_maxd), "fl_vn"},
-      {fused ? fl_fused_kernel(kind, prec, cn_maxd, vn_maxd, false) : nullptr, "fl_fused"}};
+      {fused ? fl_fused_kernel(kind, prec, cn_maxd, vn_maxd) : nullptr, "fl_fused"}};
   *bytes = 0;
   *name = "";
   for (const auto& k : ks) {

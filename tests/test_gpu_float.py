@@ -351,27 +351,3 @@ def test_fused_global_slot_index_path(eng, monkeypatch, wlan_H, prec):
     passes, it_p = _gpu(eng, g, oracle.MINSUM, 12, llr, prec, True, graph_obj=G, path="passes")
     assert it_f == it_p
     np.testing.assert_array_equal(fused, passes)
-
-
-@pytest.mark.parametrize("kind", [oracle.MINSUM, oracle.BP])
-@pytest.mark.parametrize("name,imax,B,early,ebn0", [
-    ("wlan", 10, 301, False, 1.5),     # ragged last group (odd B)
-    ("wlan", 30, 64, True, 4.0),       # batch-global stop before imax-1: pass 2 re-runs to L
-    ("reg", 12, 131, True, 3.0),
-    ("wlan1944", 8, 1001, False, 1.5)])
-def test_fused_compact_groups_equal_passes(eng, monkeypatch, kind, name, imax, B, early, ebn0, wlan_H, reg_H):
-    """Compact fp32 groups of the fused kernel (IBL_FUSED_FCW=2: 2 codewords per workgroup in 8-byte slots,
-    two workgroups per CU) equal the per-pass path bit for bit, with the same stop iteration."""
-    from informationbottleneckdecodingldpc_amd import codes
-    H = {"wlan": wlan_H, "reg": reg_H}.get(name)
-    if H is None:
-        H = codes.wlan_80211n(81)
-    g = graph.build_graph(H)
-    G = eng.Graph(g, DEV)
-    llr = _llrs(g, B, ebn0, seed=imax * 5 + B, quantised=True)
-    monkeypatch.setenv("IBL_FUSED_FCW", "2")
-    fused, it_f = _gpu(eng, g, kind, imax, llr, torch.float32, early, graph_obj=G, path="fused")
-    monkeypatch.delenv("IBL_FUSED_FCW")
-    passes, it_p = _gpu(eng, g, kind, imax, llr, torch.float32, early, graph_obj=G, path="passes")
-    assert it_f == it_p
-    np.testing.assert_array_equal(fused, passes)
