@@ -45,6 +45,11 @@ VARIANTS = {
     "cs2f": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024", 'IBL_SCHED_FILE="ib_sched_cs2f.inc"'],
     "cs2o5": ["IBL_CN_STRIDED=1", "IBL_LB8C=256", "IBL_WPE8C=5", "IBL_LB8F=1024",
               'IBL_SCHED_FILE="ib_sched_cs2o5.inc"'],
+    # one dword per lane (8 codewords) and all 8 in one check-schedule group: 16 check chains in flight
+    "w1s8": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1s8.inc"'],
+    "w1l4": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1l4.inc"'],
+    "w2l4": ['IBL_SCHED_FILE="ib_sched_w2l4.inc"'],
+    "w1": ["IBL_W=1"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
@@ -57,7 +62,7 @@ VARIANTS = {
 }
 # gen_sched.py arguments of the variants that need their own schedule file
 SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3",
-              "s2n": "2 4 2 4 0 0", "cs2": "2 4 2 4 0 0", "cs2f": "2 4 2 4 0 0", "cs2o5": "2 4 2 4 0 0"}
+              "s2n": "2 4 2 4 0 0", "cs2": "2 4 2 4 0 0", "cs2f": "2 4 2 4 0 0", "cs2o5": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0"}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
