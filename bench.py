@@ -219,7 +219,22 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
         roof["lds_lookups_per_clk_per_cu"] = {k: round(lk[k] / (avg[k] * 1e-3) / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2)
                                               for k in lk}
         roof["lds_lookups_per_clk_per_cu"]["ceiling"] = 32.0
+        mc = measured_lookup_ceiling()
+        if mc:
+            roof["lds_lookups_per_clk_per_cu"]["measured_chain_rate"] = mc
     return roof
+
+
+def measured_lookup_ceiling(path=os.path.join(ROOT, "profiles", "r03_ubench_lookup_rate.json")):
+    """Highest LDS-only lookup rate (lookups/clk/CU at the nominal clock) that tools/ubench/lookup_rate.hip
+    measured for dependent ds_read_u8 chains on the decoders' table layout (profiles/, JSON lines), or None."""
+    try:
+        with open(path) as fh:
+            rows = [json.loads(l) for l in fh if l.strip()]
+        rates = [r["lookups_per_clk_per_cu"] for r in rows if r.get("global_chains") == 0]
+        return round(max(rates), 2) if rates else None
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def aggregate_rate(B: int, steps: int, elapsed_local: float) -> dict:

@@ -121,3 +121,11 @@ def test_committed_bench_lines_are_physical():
                 assert d["roofline"]["frac"] <= 1.0, p
                 seen += 1
     assert seen >= 0
+
+
+def test_measured_lookup_ceiling_from_profile():
+    """bench.py reports the LDS lookup-chain rate the committed microbenchmark measured beside the nominal
+    32/clk/CU ceiling (LDS-only rows of profiles/r03_ubench_lookup_rate.json)."""
+    import bench
+    mc = bench.measured_lookup_ceiling()
+    assert mc is not None and 20.0 < mc <= 32.0
