@@ -98,15 +98,12 @@ int ibl_ib_path(const ibl_ib* h);
 int ibl_ib_set_path(ibl_ib* h, int32_t path);
 int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
 /*
- * Per-pass fast-path features (no reference counterpart; results are identical either way):
- * IBL_FEAT_FOLD = the check pass also applies the degree-2 variables' table and writes their outputs
- * straight into the next check inbox, and the variable pass skips those variables (codes whose checks
- * have at most 2 degree-2 neighbours and degrees <= 8, e.g. DVB-S2's staircase, WLAN's dual diagonal).
- * Opt-in with environment IBL_FOLD=1 at create: on MI355X the fold's check kernel runs out of registers
- * and the decode is slower (DESIGN.md "Degree-2 fold").
+ * Codewords per workgroup the fused kernel runs a batch of B with (no reference counterpart; results are
+ * identical either way): 8, or 4 (half groups) when 2 * ceil(B / 8) workgroups fit the grid or the
+ * environment IBL_FUSED_NCW=4 forces them and the half-group kernel fits the device; 0 when decodes do
+ * not run the fused kernel.
  */
-#define IBL_FEAT_FOLD 1
-int ibl_ib_features(const ibl_ib* h, int32_t* features);
+int ibl_ib_fused_ncw(const ibl_ib* h, int32_t B, int32_t* ncw);
 /*
  * Decode B codewords.  Replaces decode_OpenCL (discrete_LDPC_decoder_irreg.py:245-341;
  * discrete_LDPC_decoder.py:202-295).
@@ -143,6 +140,10 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
  * Replaces decode_OpenCL_min_sum (min_sum_decoder_irreg.py:221-287) and
  * decode_OpenCL_belief_propagation (bp_decoder_irreg.py:221-286).
  *   d_llr [N][B] channel LLRs (IBL_F32 / IBL_F64), d_out [N][B] APP LLRs (IBL_F32 / IBL_F64)
+ * Precondition: no channel LLR is NaN.  +-inf is allowed (a known bit: every message a variable sends
+ * is clamped to +-llr_max, its APP LLR is +-inf), and every message stays finite, so no operation
+ * creates a NaN (BP box-plus inputs are clamped, |a+b| <= 2 llr_max).  The float kernels are built
+ * for NaN-free data (-fno-honor-nans, IEEE mode off): a NaN input gives unspecified outputs.
  */
 int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out,
                      int32_t out_dtype, int32_t early_stop, int32_t* d_iters, void* stream);

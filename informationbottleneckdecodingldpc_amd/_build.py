@@ -29,9 +29,11 @@ def _stale(out: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB, tag: str = "") -> str:
-    """Compile the HIP sources and link `lib`. `defines` (e.g. ["IBL_W=2"]) select kernel variants;
-    variant objects go to build/<tag>/."""
+def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB, tag: str = "",
+          src_flags=None) -> str:
+    """Compile the HIP sources and link `lib`. `defines` (e.g. ["IBL_W=2"]) select kernel variants,
+    `src_flags` replaces SRC_FLAGS; variant objects go to build/<tag>/."""
+    src_flags = SRC_FLAGS if src_flags is None else src_flags
     objdir = os.path.join(PKG, "build", tag) if tag else os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
     headers = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "ibldpc.h")] + \
@@ -41,7 +43,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB
         s = os.path.join(CSRC, src)
         o = os.path.join(objdir, src.replace(".hip", ".o"))
         if force or _stale(o, [s] + headers):
-            jobs.append([HIPCC, *FLAGS, *SRC_FLAGS.get(src, []), *[f"-D{d}" for d in defines], "-c", s, "-o", o])
+            jobs.append([HIPCC, *FLAGS, *src_flags.get(src, []), *[f"-D{d}" for d in defines], "-c", s, "-o", o])
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):

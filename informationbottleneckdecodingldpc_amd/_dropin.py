@@ -21,9 +21,6 @@ from . import codes
 from .engine import Graph
 from .graph import build_graph
 
-_GRAPH_CACHE: dict = {}
-
-
 def resolve_device(context_) -> torch.device:
     if context_ is False or context_ is None:
         if not torch.cuda.is_available():
@@ -85,11 +82,14 @@ class CodeMixin:
         self.R_c = self.edges.R_c
 
     def _graph_on(self, dev: torch.device) -> Graph:
-        key = (id(self.edges), dev.index)
-        g = _GRAPH_CACHE.get(key)
+        """The device copy of the edge arrays, one per device, held by this decoder only: it is freed with
+        the decoder (``Graph.__del__``), so constructing decoders per Eb/N0 point or per code does not
+        accumulate device memory."""
+        graphs = self.__dict__.setdefault("_device_graphs", {})
+        g = graphs.get(dev.index)
         if g is None or g.edges is not self.edges:
             g = Graph(self.edges, dev)
-            _GRAPH_CACHE[key] = g
+            graphs[dev.index] = g
         return g
 
 

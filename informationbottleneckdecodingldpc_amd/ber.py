@@ -11,15 +11,17 @@ all-zero codewords sampled ON the device, decoded, and their decided 1-bits coun
 BER > ``target_error_rate`` and Eb/N0 < ``EbN0_dB_max_value`` (:156-163). Results are saved as the
 reference's ``BER_results.npz`` keys (``EbN0_dB_vector``, ``BER_vector``).
 
-Multi-GPU: one process per GPU (torch.distributed initialised by the caller); rank r draws its
-channel from Philox key ``seed + r`` (disjoint streams), and the error / block counters are summed
-over ranks (one small all-reduce per ``sync_every`` batches) so every rank stops at the same point.
-``max_blocks`` bounds a point (the reference loops until ``min_errors`` however long that takes).
+Multi-GPU: one process per GPU (torch.distributed initialised by the caller). Batches are dealt
+round-robin and every batch's channel is keyed on its GLOBAL batch index (``global_batch``), the error
+counts of each round are exchanged (one small all-reduce per ``sync_every`` rounds) and walked in global
+order with the reference's stop rule, so a k-rank sweep counts exactly the frames of the 1-rank sweep
+(SURVEY H9). ``max_blocks`` bounds a point (the reference loops until ``min_errors`` however long that
+takes).
 
 ``encoded=True`` transmits random encoded codewords instead (the reference's
 ``LDPC_BPSK_Transmitter`` + encoder path, AWGN_Channel_Transmission/LDPC_Transmitter.py:109-125): bits
-from the device Philox stream (key ``(seed + rank, 1)``, disjoint from the channel's ``(seed + rank, 0)``),
-batched device encoding, the channel mirrored by
+from the device Philox stream (key ``(seed, 1)``, disjoint from the channel's ``(seed, 0)``; counter keyed
+on the global batch index like the channel), batched device encoding, the channel mirrored by
 the codeword bits, and decided bits compared with the transmitted ones (``ibl_count_errors``) over the
 rows ``return_errors_all_zero`` counts.
 """
@@ -32,7 +34,7 @@ from typing import Callable, List, Optional
 
 import numpy as np
 
-__all__ = ["BERConfig", "BERResult", "run_ber", "decoder_kind"]
+__all__ = ["BERConfig", "BERResult", "run_ber", "run_ber_lockstep", "global_batch", "decoder_kind"]
 
 
 @dataclass
@@ -82,101 +84,136 @@ def decoder_kind(decoder) -> str:
     raise TypeError(f"not a decoder class: {type(decoder).__name__}")
 
 
-def _allreduce(vals):
+def _dist_world():
+    """(rank, world) of the initialised process group, else (0, 1)."""
     try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover
+        return 0, 1
+    if not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(), dist.get_world_size()
+
+
+def _dist_exchange(rank: int, world: int):
+    """Exchange for one process per rank: every rank's per-batch error counts of one round, as a
+    [world][k] list, through one all-reduce of a zero-padded float64 vector (integer counts < 2^53 add
+    exactly). RCCL (``nccl``) reduces a device tensor, gloo a host one."""
+    def exchange(local):
+        if world == 1:
+            return [list(local)]
         import torch
         import torch.distributed as dist
-    except ImportError:  # pragma: no cover
-        return vals
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
-        return vals
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
-    dist.all_reduce(t)
-    return [float(x) for x in t.cpu().tolist()]
+        k = len(local)
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.zeros(world * k, dtype=torch.float64, device=dev)
+        t[rank * k:(rank + 1) * k] = torch.tensor([float(v) for v in local], dtype=torch.float64)
+        dist.all_reduce(t)
+        v = t.cpu().tolist()
+        return [v[r * k:(r + 1) * k] for r in range(world)]
+    return exchange
 
 
-def _rank() -> int:
-    try:
-        import torch.distributed as dist
-        return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
-    except ImportError:  # pragma: no cover
-        return 0
+def global_batch(base: int, round_: int, rank: int, world: int) -> int:
+    """Global index of the batch rank ``rank`` of ``world`` decodes in its local round ``round_`` of a point
+    whose first global batch is ``base``: batches are dealt round-robin, g = base + round * world + rank, so
+    the global order (rank 0's round 0, rank 1's round 0, ..., rank 0's round 1, ...) is the 1-rank order."""
+    return int(base) + int(round_) * int(world) + int(rank)
 
 
-def run_ber(decoder, cfg: BERConfig, quantizer_factory: Optional[Callable] = None,
-            log: Optional[Callable[[str], None]] = None) -> BERResult:
-    """Run the Eb/N0 sweep with ``decoder`` (a drop-in decoder instance). ``quantizer_factory(sigma_n2)``
-    returns a quantiser object with the reference methods (default: :class:`.awgn_quantizer.AWGN_Channel_Quantizer`
-    with ``cfg.cardinality_T_channel`` clusters)."""
+def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: int, log):
+    """The Eb/N0 sweep of one rank as a generator: it yields the error counts of the batches it decoded in
+    one exchange (``sync_every`` rounds) and is sent back the [world][sync_every] counts of every rank.
+
+    Channel (and, in encoded mode, bit) streams are keyed on the GLOBAL batch index g (``global_batch``):
+    batch g's Philox counter starts at g * philox_blocks(N, B) under key ``cfg.seed`` — the reference draws
+    one stream per batch (AWGN_Quantizer_BPSK.py:201-248) and so does the 1-rank run, batch after batch.
+    Each rank then walks the exchanged counts in global order and applies the reference's loop condition
+    (``while errors < min_errors``, ``DVB-S2/BER_simulation_OpenCL.py:115-121``, plus ``max_blocks``)
+    before each batch; the batches after the stop are discarded (at most world * sync_every - 1 per point)
+    and the next point starts at the first unused global index. A k-rank sweep therefore counts exactly the
+    frames, errors and blocks of the 1-rank sweep with the same per-rank batch, whatever k and
+    ``sync_every`` are."""
     from .awgn_quantizer import AWGN_Channel_Quantizer
+    from .engine import philox_blocks
     kind = decoder_kind(decoder)
     N_var = int(decoder.codeword_len)
     R_c = float(decoder.R_c)
-    rank = _rank()
+    B = int(cfg.msg_at_time)
+    S = max(1, int(cfg.sync_every))
     if quantizer_factory is None:
         def quantizer_factory(s2):
             return AWGN_Channel_Quantizer(s2, cfg.AD_max_abs, cfg.cardinality_T_channel, cfg.cardinality_Y_channel)
     ebn0 = [float(cfg.EbN0_dB_start)]
     ber: List[float] = [0.0]
     res = BERResult(np.array([]), np.array([]))
-    offset = 0
+    pb_ch = philox_blocks(N_var, B)
+    base = 0                                    # first global batch of the current point
     tx = None
     if cfg.encoded:
         import torch
         from .engine import count_errors
         from .ldpc_encoder import LDPC_BPSK_Transmitter
-        tx = LDPC_BPSK_Transmitter(decoder.H_sparse, cfg.msg_at_time, seed=int(cfg.seed) + rank,
-                                   device=getattr(decoder, "device", None))
+        tx = LDPC_BPSK_Transmitter(decoder.H_sparse, B, seed=int(cfg.seed), device=getattr(decoder, "device", None))
+        pb_bits = philox_blocks(tx.K, B)
         # rows return_errors_all_zero counts: all N for the regular IB class (:297-300), data_len otherwise
         err_rows = N_var if type(decoder).__name__ == "Discrete_LDPC_Decoder_class" else int(decoder.data_len)
         thr = decoder.cardinality_T_decoder_ops // 2 if kind == "ib" else 0.0
         cnt = torch.zeros(1, dtype=torch.int64, device=tx.encoder.device)
+
+    def more(errors, blocks):
+        return errors < cfg.min_errors and (cfg.max_blocks is None or blocks < cfg.max_blocks)
+
     while True:
         EbN0_dB = ebn0[-1]
         sigma_n2 = 10 ** (-EbN0_dB / 10) / (2 * R_c)
         quanti = quantizer_factory(sigma_n2)
-        quanti.seed = int(cfg.seed) + rank
-        quanti.offset = offset
-        quanti.init_OpenCL_quanti(N_var, cfg.msg_at_time, return_buffer_only=True,
-                                  context_=getattr(decoder, "device", None))
-        decoder.init_OpenCL_decoding(cfg.msg_at_time, quanti.context)
-        errors = 0.0
-        blocks = 0
-        pend_err = pend_blk = 0
-        nb = 0
+        quanti.seed = int(cfg.seed)
+        quanti.offset = base * pb_ch
+        quanti.init_OpenCL_quanti(N_var, B, return_buffer_only=True, context_=getattr(decoder, "device", None))
+        decoder.init_OpenCL_decoding(B, quanti.context)
+        errors, blocks, used, rnd = 0.0, 0, 0, 0
         t0 = time.time()
-        while errors < cfg.min_errors and (cfg.max_blocks is None or blocks < cfg.max_blocks):
-            kw = {} if tx is None else {"bits": tx.transmit_bits()}
-            if kind == "ib":
-                rec = quanti.quantize_direct_OpenCL(N_var, cfg.msg_at_time, **kw)
-                dec = decoder.decode_OpenCL(rec, buffer_in=True, return_buffer=True)
-            else:
-                rec = quanti.quantize_direct_OpenCL_LLR(N_var, cfg.msg_at_time, dtype=cfg.llr_dtype, **kw)
-                fn = decoder.decode_OpenCL_min_sum if kind == "minsum" else decoder.decode_OpenCL_belief_propagation
-                dec = fn(rec, buffer_in=True, return_buffer=True)
-            if tx is None:
-                pend_err += decoder.return_errors_all_zero(dec)
-            else:
-                pend_err += int(count_errors(dec.contiguous(), err_rows, thr, kw["bits"], cnt).item())
-            pend_blk += cfg.msg_at_time
-            nb += 1
-            if nb % max(1, cfg.sync_every) == 0:
-                e, b = _allreduce([pend_err, pend_blk])
-                errors += e              # integer counts, summed exactly in float64
-                blocks += int(round(b))
-                pend_err = pend_blk = 0
-        if pend_blk:
-            e, b = _allreduce([pend_err, pend_blk])
-            errors += e
-            blocks += int(round(b))
-        offset = quanti.offset
+        while more(errors, blocks):
+            local = []
+            for s in range(S):
+                g = global_batch(base, rnd + s, rank, world)
+                kw = {}
+                if tx is not None:
+                    tx.offset = g * pb_bits
+                    kw["bits"] = tx.transmit_bits()
+                quanti.offset = g * pb_ch
+                if kind == "ib":
+                    rec = quanti.quantize_direct_OpenCL(N_var, B, **kw)
+                    dec = decoder.decode_OpenCL(rec, buffer_in=True, return_buffer=True)
+                else:
+                    rec = quanti.quantize_direct_OpenCL_LLR(N_var, B, dtype=cfg.llr_dtype, **kw)
+                    fn = decoder.decode_OpenCL_min_sum if kind == "minsum" else decoder.decode_OpenCL_belief_propagation
+                    dec = fn(rec, buffer_in=True, return_buffer=True)
+                if tx is None:
+                    local.append(float(decoder.return_errors_all_zero(dec)))
+                else:
+                    local.append(float(count_errors(dec.contiguous(), err_rows, thr, kw["bits"], cnt).item()))
+            counts = yield local
+            stop = False
+            for s in range(S):                  # global order: round-major, rank-minor
+                for r in range(world):
+                    if not more(errors, blocks):
+                        stop = True
+                        break
+                    errors += counts[r][s]      # integer counts, summed exactly in float64
+                    blocks += B
+                    used += 1
+                if stop:
+                    break
+            rnd += S
+        base += used
         spent = time.time() - t0
         ber[-1] = errors / (R_c * blocks * N_var) if blocks else 0.0
         res.errors.append(errors)
         res.blocks.append(blocks)
         res.seconds.append(spent)
-        if log:
+        if log and rank == 0:
             log(f"EbN0_dB={EbN0_dB:.3f} BER={ber[-1]:.3e} errors={errors:.0f} blocks={blocks} "
                 f"bitrate={R_c * blocks * N_var / max(spent, 1e-9):.3e} bit/s")
         if ber[-1] > cfg.target_error_rate and EbN0_dB < cfg.EbN0_dB_max_value:
@@ -189,3 +226,57 @@ def run_ber(decoder, cfg: BERConfig, quantizer_factory: Optional[Callable] = Non
     res.EbN0_dB_vector = np.asarray(ebn0)
     res.BER_vector = np.asarray(ber)
     return res
+
+
+def _drive(gens, exchange):
+    """Run rank generators in lockstep: each round's local counts go through ``exchange`` (a list of the
+    gens' lists -> the [world][k] matrix) and the matrix is sent back to every gen."""
+    locals_ = [next(g) for g in gens]
+    while True:
+        counts = exchange(locals_)
+        nxt, done = [], []
+        for g in gens:
+            try:
+                nxt.append(g.send(counts))
+            except StopIteration as e:
+                done.append(e.value)
+        if done:
+            if len(done) != len(gens):
+                raise RuntimeError("ranks of a BER sweep disagree on when to stop")
+            return done
+        locals_ = nxt
+
+
+def run_ber(decoder, cfg: BERConfig, quantizer_factory: Optional[Callable] = None,
+            log: Optional[Callable[[str], None]] = None, rank: Optional[int] = None,
+            world: Optional[int] = None) -> BERResult:
+    """Run the Eb/N0 sweep with ``decoder`` (a drop-in decoder instance). ``quantizer_factory(sigma_n2)``
+    returns a quantiser object with the reference methods (default: :class:`.awgn_quantizer.AWGN_Channel_Quantizer`
+    with ``cfg.cardinality_T_channel`` clusters). ``rank`` / ``world`` default to the initialised process
+    group (one process per GPU; counters exchanged by all-reduce) or (0, 1). The result is the same for
+    every world size (see ``_rank_sweep``); :func:`run_ber_lockstep` emulates k ranks in one process."""
+    r0, w0 = _dist_world()
+    rank = r0 if rank is None else int(rank)
+    world = w0 if world is None else int(world)
+    if world > 1 and w0 != world:
+        raise ValueError(f"world={world} needs an initialised process group of that size (have {w0}); "
+                         "use run_ber_lockstep to emulate ranks in one process")
+    gen = _rank_sweep(decoder, cfg, quantizer_factory, rank, world, log)
+    ex = _dist_exchange(rank, world)
+    return _drive([gen], lambda loc: ex(loc[0]))[0]
+
+
+def run_ber_lockstep(decoders, cfg: BERConfig, world: int, quantizer_factory: Optional[Callable] = None,
+                     log: Optional[Callable[[str], None]] = None) -> BERResult:
+    """``world`` ranks of a multi-GPU sweep emulated in one process: rank r decodes its global batches with
+    ``decoders[r]`` (or one shared decoder; a decode call is self-contained), rounds run in lockstep and
+    the counts are exchanged in memory. Returns rank 0's result (every rank's is checked equal)."""
+    decs = list(decoders) if isinstance(decoders, (list, tuple)) else [decoders] * int(world)
+    if len(decs) != world:
+        raise ValueError("one decoder per rank")
+    gens = [_rank_sweep(decs[r], cfg, quantizer_factory, r, world, log) for r in range(world)]
+    out = _drive(gens, lambda loc: [list(x) for x in loc])
+    for o in out[1:]:
+        if o.errors != out[0].errors or o.blocks != out[0].blocks:
+            raise RuntimeError("emulated ranks disagree")
+    return out[0]

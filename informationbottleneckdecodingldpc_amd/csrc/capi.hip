@@ -71,28 +71,16 @@ struct ibl_graph {
   std::vector<int32_t> h_cn_deg, h_vn_deg;
   int32_t *cn_start = nullptr, *cn_deg = nullptr, *tgt_cn = nullptr;
   int32_t *vn_start = nullptr, *vn_deg = nullptr, *tgt_vn = nullptr, *csr_cols = nullptr;
-  // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable); the check
-  // order's 4th word is the mask of edge positions whose variable has degree 2 (degree-2 fold)
+  // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable)
   int32_t *cn_info = nullptr, *vn_info = nullptr;
   int32_t cn_heavy = 0, vn_heavy = 0;
-  // degree-2 fold (IbFastArgs::fold_mode): the variable work order without the degree-2 variables, the
-  // CSR edge of each degree-2 variable's other check, and whether every check has at most 2 of them
-  int32_t *vn_info_nf = nullptr, *fold_other = nullptr;
-  int32_t n_v_nf = 0, vn_heavy_nf = 0, n_deg2 = 0;
-  bool fold_ok = false;
 };
 
 namespace {
-// skip (optional): nodes left out of the order (the degree-2 variables of the fold's variable order);
-// word3 (optional): the 4th word of each node's record
-std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::vector<int32_t>& deg, int32_t* heavy,
-                                const std::function<bool(int32_t)>& skip = nullptr,
-                                const std::vector<int32_t>* word3 = nullptr) {
+std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::vector<int32_t>& deg, int32_t* heavy) {
   const int32_t n = (int32_t)deg.size();
-  std::vector<int32_t> idx;
-  idx.reserve(n);
-  for (int32_t i = 0; i < n; ++i)
-    if (!skip || !skip(i)) idx.push_back(i);
+  std::vector<int32_t> idx(n);
+  for (int32_t i = 0; i < n; ++i) idx[i] = i;
   std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
   std::vector<int32_t> info(idx.size() * 4);
   *heavy = 0;
@@ -101,7 +89,7 @@ std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::ve
     info[4 * p] = v;
     info[4 * p + 1] = start[v];
     info[4 * p + 2] = deg[v];
-    info[4 * p + 3] = word3 ? (*word3)[v] : 0;
+    info[4 * p + 3] = 0;
     if (deg[v] > kLightD) ++*heavy;
   }
   return info;
@@ -174,12 +162,6 @@ struct ibl_ib {
   int cn_ncs = 0, vn_ncs = 0;
   int8_t cn_ccol[kMaxD + 1][4] = {{0}}, vn_ccol[kMaxD + 1][4] = {{0}};
   KCfg kcn, kvn, kdec;
-  // degree-2 fold of the per-pass fast path (IbFastArgs::fold_mode): second check inbox, the fold table's
-  // LDS slot in the check images, the fold check kernel's launch configuration
-  bool fold = false;
-  uint8_t* cin2 = nullptr;
-  int32_t cn_fold_slot = 0;
-  KCfg kcnf;
   KTimer timer;
   // fused on-chip path (IbFusedArgs, short codes): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
@@ -284,33 +266,12 @@ int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int3
   g->dvm = *std::max_element(vd.begin(), vd.end());
   g->h_cn_deg = cd;
   g->h_vn_deg = vd;
-  // degree-2 fold: per check the mask of edge positions with a degree-2 variable, per CSR edge of such
-  // a variable the CSR edge of its other check
-  std::vector<int32_t> fmask(n_c, 0), fother(E, -1);
-  g->fold_ok = g->dcm <= 8;
-  for (int32_t c = 0; c < n_c; ++c) {
-    int cnt = 0;
-    for (int32_t e = cs[c]; e < cs[c] + cd[c]; ++e) {
-      const int32_t v = cols[e];
-      if (vd[v] != 2) continue;
-      fmask[c] |= 1 << (e - cs[c]);
-      fother[e] = tv[vs[v]] == e ? tv[vs[v] + 1] : tv[vs[v]];
-      ++cnt;
-    }
-    if (cnt > 2) g->fold_ok = false;
-  }
-  for (int32_t v = 0; v < n_v; ++v) g->n_deg2 += vd[v] == 2;
-  std::vector<int32_t> vinf = work_order(vs, vd, &g->vn_heavy_nf, [&](int32_t v) { return vd[v] == 2; });
-  g->n_v_nf = (int32_t)(vinf.size() / 4);
-  if (vinf.empty()) vinf.assign(4, 0);
   if ((rc = dupload(&g->cn_start, cs.data(), n_c)) || (rc = dupload(&g->cn_deg, cd.data(), n_c)) ||
       (rc = dupload(&g->tgt_cn, tc.data(), E)) || (rc = dupload(&g->vn_start, vs.data(), n_v)) ||
       (rc = dupload(&g->vn_deg, vd.data(), n_v)) || (rc = dupload(&g->tgt_vn, tv.data(), E)) ||
       (rc = dupload(&g->csr_cols, cols, E)) ||
-      (rc = dupload(&g->cn_info, work_order(cs, cd, &g->cn_heavy, nullptr, &fmask).data(), (size_t)n_c * 4)) ||
-      (rc = dupload(&g->vn_info, work_order(vs, vd, &g->vn_heavy).data(), (size_t)n_v * 4)) ||
-      (rc = dupload(&g->vn_info_nf, vinf.data(), vinf.size())) ||
-      (rc = dupload(&g->fold_other, fother.data(), E))) {
+      (rc = dupload(&g->cn_info, work_order(cs, cd, &g->cn_heavy).data(), (size_t)n_c * 4)) ||
+      (rc = dupload(&g->vn_info, work_order(vs, vd, &g->vn_heavy).data(), (size_t)n_v * 4))) {
     ibl_graph_destroy(g);
     return rc;
   }
@@ -333,7 +294,7 @@ void ibl_graph_destroy(ibl_graph* g) {
   (void)hipSetDevice(g->device);
   dfree(g->cn_start); dfree(g->cn_deg); dfree(g->tgt_cn);
   dfree(g->vn_start); dfree(g->vn_deg); dfree(g->tgt_vn); dfree(g->csr_cols);
-  dfree(g->cn_info); dfree(g->vn_info); dfree(g->vn_info_nf); dfree(g->fold_other);
+  dfree(g->cn_info); dfree(g->vn_info);
   delete g;
 }
 
@@ -408,6 +369,19 @@ int pick_cfg(int which, int maxd, int nt, int ncs, int num_cus, KCfg* k) {
 
 int ib_fused_setup(ibl_ib* h);           // fused on-chip IB decoder (defined with the float one below)
 bool ib_fused_in_use(const ibl_ib* h);
+
+// Codewords per workgroup of the fused IB kernel for a batch of B: 4-codeword half groups when even the
+// doubled number of workgroups fits the grid (each half group then has a workgroup slot of its own);
+// whole 8-codeword groups otherwise — with 2*ngroups > grid some workgroups would run two half groups in
+// a row, and a half group takes more than half a group's time (per-phase latency). The
+// environment IBL_FUSED_NCW=8 / 4 forces either (A/B, tests); 4 needs the half-group kernel (f_half_ok).
+int ib_fused_ncw(const ibl_ib* h, int B) {
+  const int ngroups = (B + 7) / 8;
+  const char* e = getenv("IBL_FUSED_NCW");
+  const int forced = e ? atoi(e) : 0;
+  if (!h->f_half_ok || forced == 8) return 8;
+  return (forced == 4 || 2 * ngroups <= h->f_grid) ? 4 : 8;
+}
 }  // namespace
 
 extern "C" {
@@ -464,14 +438,6 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     cn_nt += (int)cdeg.size();
     for (int d : vdeg) vn_nt += (d >= 2);
   }
-  // degree-2 fold (fast path, check degrees <= 8, at most 2 degree-2 variables per check): one more check
-  // table per pass, the next variable pass's degree-2 table. Opt-in (IBL_FOLD=1): measured on DVB-S2 (C4)
-  // the variable pass drops from 0.447 to 0.337 ms but the fold check kernel needs more than the 128 VGPRs
-  // of a 1024-thread block (768 threads: 0.677 ms; 1024 with scratch spills: 0.600; plain 0.478), so the
-  // decode is slower (158.7k / 171.0k vs 173.8k cw/s, DESIGN.md "Degree-2 fold")
-  const char* fe = getenv("IBL_FOLD");
-  const bool want_fold = g->fold_ok && g->n_deg2 > 0 && imax > 1 && fe && fe[0] == '1';
-  if (want_fold) ++cn_nt;
   const int max_nt = (kLdsBytes / kRegion) * 4;
   // table slot of each column-fetched input (cn_ncols / vn_ncols): raw fold table, or the degree's
   // final (matching-composed) table; slots are numbered as in the pass images below
@@ -536,15 +502,6 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
         else tbs.push_back(make_table(T, [&](int t, int m) { return match_cn[mrow + cn_raw(p, d - 3, t, m)]; }));
         h->cn_fslot[d] = slot++;
       }
-      if (want_fold) {   // the degree-2 variable table of variable pass p (none after the last check pass)
-        const int64_t mrow = (int64_t)p * T * VM + (int64_t)(2 - 1) * T;
-        const bool has = p < imax - 1;
-        tbs.push_back(make_table(T, [&](int t, int m) {
-          const int raw = has ? vn_raw(p, 0, t, m) : 0;
-          return has && h->match ? match_vn[mrow + raw] : raw;
-        }));
-        h->cn_fold_slot = (int32_t)tbs.size() - 1;
-      }
       append_pass(cimg, tbs, regions_of(cn_nt));
       append_cols(ccimg, tbs, ccol_slot);
     }
@@ -582,19 +539,13 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
         (rc = pick_cfg(1, VM, 4 * h->vn_nt, h->vn_ncs, g->num_cus, &h->kvn)) ||
         (rc = pick_cfg(2, VM, 4 * h->dec_nt, 0, g->num_cus, &h->kdec)))
       return bail(rc);
-    h->fold = want_fold && h->cn_ncs == 0;
-    if (h->fold) {
-      if ((rc = pick_cfg(3, CM, 4 * h->cn_nt, 0, g->num_cus, &h->kcnf)) || (rc = dalloc(&h->cin2, inbox)))
-        return bail(rc);
-      if (hipMemset(h->cin2, 0, inbox) != hipSuccess) return bail(fail(IBL_EHIP, "hipMemset failed"));
-    }
     // The fast kernels are built to run without a private segment (launch bounds sized to the node
     // bodies' registers, item buffers forced inline). A build whose compiler spills registers or passes
     // an item through scratch would silently lose the register budget the design rests on, and such a
     // build once faulted (DESIGN.md "Private segment"): refuse it loudly instead.
     size_t priv = 0;
     const char* kname = "";
-    HIPCHK(ib_fast_private_bytes(CM, VM, h->fold, &priv, &kname));
+    HIPCHK(ib_fast_private_bytes(CM, VM, &priv, &kname));
     if (priv != 0 && !getenv("IBL_ALLOW_SCRATCH"))   // diagnostics only (the spill experiment)
       return bail(fail(IBL_EHIP, std::string("fast-path kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill / scratch item): rebuild required"));
@@ -613,11 +564,6 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
 
 int ibl_ib_path(const ibl_ib* h) { return h && h->fast ? 1 : 0; }
 
-int ibl_ib_features(const ibl_ib* h, int32_t* features) {
-  if (!h || !features) return fail(IBL_EINVAL, "decoder or features is NULL");
-  *features = h->fold ? IBL_FEAT_FOLD : 0;
-  return IBL_OK;
-}
 
 int ibl_ib_set_path(ibl_ib* h, int32_t path) {
   if (!h) return fail(IBL_EINVAL, "decoder is NULL");
@@ -627,6 +573,13 @@ int ibl_ib_set_path(ibl_ib* h, int32_t path) {
     return fail(IBL_EUNSUPPORTED, "code does not fit the fused IB kernel (fast path, E * 4 B of messages plus the "
                                   "largest pass's tables within 160 KiB, check degrees >= 2)");
   h->path = path;
+  return IBL_OK;
+}
+
+int ibl_ib_fused_ncw(const ibl_ib* h, int32_t B, int32_t* ncw) {
+  if (!h || !ncw) return fail(IBL_EINVAL, "NULL argument");
+  if (B < 1 || B > h->max_batch) return fail(IBL_EINVAL, "B must lie in [1, max_batch]");
+  *ncw = ib_fused_in_use(h) ? ib_fused_ncw(h, B) : 0;
   return IBL_OK;
 }
 
@@ -658,7 +611,7 @@ int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_n, double* vn
 void ibl_ib_destroy(ibl_ib* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
-  dfree(h->cin); dfree(h->cin2); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
+  dfree(h->cin); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
   dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img); dfree(h->cn_cimg); dfree(h->vn_cimg);
   dfree(h->cn_lut); dfree(h->vn_lut); dfree(h->mc); dfree(h->mv);
   dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
@@ -695,11 +648,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     const size_t esz = out_dtype == kU8 ? 1 : 4;
     f.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
     f.ngroups = (B + 7) / 8;
-    // half groups (4 codewords per workgroup) when whole groups would leave workgroup slots idle;
-    // IBL_FUSED_NCW=8 / 4 forces either (A/B, tests)
-    const char* ncwe = getenv("IBL_FUSED_NCW");
-    const int ncw_env = ncwe ? atoi(ncwe) : 0;
-    f.ncw = (h->f_half_ok && (ncw_env == 4 || (ncw_env != 8 && f.ngroups < h->f_grid))) ? 4 : 8;
+    f.ncw = ib_fused_ncw(h, B);
     const int grid = std::min(h->f_grid, f.ngroups * (8 / f.ncw));
     // diagnostics: IBL_TRACE_FUSED=<file> records block 0's clock at every phase boundary of its first group
     const char* ftrace = getenv("IBL_TRACE_FUSED");
@@ -733,19 +682,11 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     const int ldbb = h->ldb / 2;
     HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     IbFastArgs cn{}, vn{};
-    // degree-2 fold: check inbox buffers C[0], C[1] — check pass j reads C[j % 2]; its folded degree-2
-    // outputs and the following variable pass (which skips the degree-2 variables) write C[(j + 1) % 2].
-    // The last check pass writes every varnode-inbox row (the decision reads them); under early stop every
-    // pass does (any may be the last).
-    const bool fold = h->fold;
-    uint8_t* const cbuf[2] = {h->cin, fold ? h->cin2 : h->cin};
-    auto fold_mode_of = [&](int j) { return !fold || j == I - 1 ? 0 : (early ? 2 : 1); };
     cn.ch8 = vn.ch8 = h->ch8;
     cn.info = g->cn_info; cn.tgt = g->tgt_cn; cn.out = h->vin;
-    vn.info = fold ? g->vn_info_nf : g->vn_info; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
-    cn.n_nodes = g->n_c; vn.n_nodes = fold ? g->n_v_nf : g->n_v;
-    cn.n_heavy = g->cn_heavy; vn.n_heavy = fold ? g->vn_heavy_nf : g->vn_heavy;
-    cn.fold_slot = h->cn_fold_slot; cn.fold_other = g->fold_other; cn.fold_var = g->csr_cols;
+    vn.info = g->vn_info; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
+    cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.n_heavy = g->cn_heavy; vn.n_heavy = g->vn_heavy;
     cn.nchunks = (B + ccn - 1) / ccn;
     vn.nchunks = (B + cvn - 1) / cvn;
     cn.ldb = vn.ldb = ldbb;
@@ -761,19 +702,14 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     // pass 0: send + checknode_update_iter0, inputs gathered from the staged channel rows
     cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
     cn.cimg = h->cn_cimg;
-    auto launch_cn = [&]() {
-      const KCfg& k = cn.fold_mode ? h->kcnf : h->kcn;
-      return launch_ib_cn_fast(cn, h->CM, k.grid, k.block, k.lds, s);
-    };
-    cn.fold_mode = fold_mode_of(0);
-    cn.fold_out = cbuf[1];
+    auto launch_cn = [&]() { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); };
     HIPCHK(h->timer.timed(0, s, launch_cn));
     cn.gather = nullptr;
     // diagnostics: IBL_TRACE_WAVES=<prefix> records {start, end, items|cu} of every wave of the middle
     // iteration's VN and CN launches into <prefix>_vn.bin / <prefix>_cn.bin (uint64 triples)
     const char* trace_path = getenv("IBL_TRACE_WAVES");
     uint64_t* trace = nullptr;
-    const size_t nwv = (size_t)h->kvn.grid * (h->kvn.block / 64), nwc = std::max((size_t)h->kcn.grid * (h->kcn.block / 64), (size_t)h->kcnf.grid * (h->kcnf.block / 64));
+    const size_t nwv = (size_t)h->kvn.grid * (h->kvn.block / 64), nwc = (size_t)h->kcn.grid * (h->kcn.block / 64);
     if (trace_path && I > 1) HIPCHK(hipMalloc((void**)&trace, sizeof(uint64_t) * 3 * (nwv + nwc)));
     for (int j = 1; j < I; ++j) {
       const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
@@ -781,16 +717,13 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
       vn.cimg = h->vn_cimg + (size_t)(j - 1) * h->vn_ncs * 32;
       vn.gate = gate;
       vn.trace = (trace && j == I / 2) ? trace : nullptr;
-      vn.out = cbuf[j % 2];
       HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_fast(vn, h->VM, h->kvn.grid, h->kvn.block, h->kvn.lds, s); }));
       cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
       cn.cimg = h->cn_cimg + (size_t)j * h->cn_ncs * 32;
       cn.gate = gate;
       cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
       cn.trace = (trace && j == I / 2) ? trace + 3 * nwv : nullptr;
-      cn.in = cbuf[j % 2];
-      cn.fold_out = cbuf[(j + 1) % 2];
-      cn.fold_mode = fold_mode_of(j);
+      cn.in = h->cin;
       HIPCHK(h->timer.timed(0, s, launch_cn));
     }
     if (trace) {

@@ -91,14 +91,6 @@ struct IbFastArgs {
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
   uint64_t* trace;          // diagnostics (IBL_TRACE_WAVES): per wave {start clock, end clock, items}, else nullptr
-  // degree-2 variable fold (check pass only; info[4*pos+3] = mask of the node's edge positions whose
-  // variable has degree 2, at most 2 per check): the pass also applies the next variable pass's degree-2
-  // table to those outputs and writes the result straight into the next check-inbox buffer
-  int32_t fold_mode;        // 0 off; 1 fold only (no varnode-inbox row for those edges); 2 fold + varnode row
-  int32_t fold_slot;        // LDS table slot of the degree-2 variable table (final, matching composed)
-  uint8_t* fold_out;        // next check-inbox buffer [E][ldb]
-  const int32_t* fold_other;// CSR edge -> the CSR edge of its degree-2 variable's other check (-1: none)
-  const int32_t* fold_var;  // CSR edge -> variable (csr_cols), for the channel row
 };
 
 struct IbDecArgs {
@@ -232,7 +224,7 @@ hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t ld
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu);
 // Largest private (scratch) segment over the fast-path kernels a decoder of max degree maxd launches
 // (CN with and without gather, VN, decision); *name receives that kernel's name.
-hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, bool fold, size_t* bytes, const char** name);
+hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name);
 hipError_t launch_ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm, uint32_t* chT,
                              hipStream_t s);
 hipError_t launch_ib_fused(const IbFusedArgs& a, int cmax, int vmax, int grid, int block, size_t lds, hipStream_t s);

@@ -118,19 +118,6 @@ template <> struct RowVec<4> { typedef uint4 T; };
 #ifndef IBL_NT
 #define IBL_NT 1
 #endif
-// Check-pass word layout. IBL_CN_STRIDED = 1: lane l's word i of a row segment is dword i*64 + l (each
-// row access of the wave is W fully coalesced 256-B dword accesses), so the check node stores word i's D
-// outputs as soon as they exist: no D x W output array stays live across the next word's lookups (-8
-// VGPRs at D = 7, W = 2). 0: lane l owns the W consecutive dwords W*l.. (one dwordxW access per row).
-// The variable pass keeps its own (contiguous) assignment: a row's byte format is the same either way.
-#ifndef IBL_CN_STRIDED
-#define IBL_CN_STRIDED 0
-#endif
-// IBL_FOLD_LATE (contiguous layout only): request the fold rows' channel words after the node's lookups
-// instead of before them (4 fewer VGPRs live across the body; the loads' latency is then exposed)
-#ifndef IBL_FOLD_LATE
-#define IBL_FOLD_LATE 0
-#endif
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 template <int W> struct RowNV;
@@ -182,16 +169,6 @@ __device__ __forceinline__ void store_row(uint8_t* p, const uint32_t (&r)[W]) {
   }
 }
 
-template <int W, bool STRIDED>
-__device__ __forceinline__ void load_words(const uint8_t* p, uint32_t (&r)[W]) {
-  if constexpr (STRIDED) {
-#pragma unroll
-    for (int i = 0; i < W; ++i) r[i] = *reinterpret_cast<const uint32_t*>(p + 256 * i);
-  } else {
-    load_row<W>(p, r);
-  }
-}
-__device__ __forceinline__ void store_word(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
 
 // A wave item's inputs, fetched one item ahead of its computation (register double buffer):
 // the row loads of item k+1 are issued before item k is computed, so HBM latency overlaps the
@@ -213,7 +190,6 @@ struct ItemBuf {
   int d, st, node;
   uint32_t off;            // byte offset of this lane's words in a row
   int cwb;                 // first codeword of this lane
-  int fm;                  // check pass: edge positions with a degree-2 variable (info[4*pos+3])
 };
 
 // Items of a phase: item = first + (pos - pos0) * nch + chunk (nch chunks of 512*W codewords per node)
@@ -221,7 +197,7 @@ struct PhaseItems {
   int first, pos0, nch;
 };
 
-template <class Buf, bool VN, bool GATHER, bool FOLD = false>
+template <class Buf, bool VN, bool GATHER>
 __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int lane, Buf& b, const PhaseItems& pi) {
   constexpr int W = Buf::W, MAXD = Buf::kMax;
   const int rel = item - pi.first;
@@ -232,18 +208,15 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   b.node = node;
   b.st = sload(a.info, 4 * pos + 1);
   b.d = sload(a.info, 4 * pos + 2);
-  b.fm = VN ? 0 : sload(a.info, 4 * pos + 3);
-  constexpr bool ST = !VN && IBL_CN_STRIDED;   // check-pass word layout (see cn_compute)
-  b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * (ST ? 1 : W));
-  b.cwb = chunk * (512 * W) + lane * 8 * (ST ? 1 : W);
+  b.off = (uint32_t)(chunk * (256 * W) + lane * 4 * W);
+  b.cwb = chunk * (512 * W) + lane * 8 * W;
   // always MAXD loads (rows past the degree repeat the last row and hit in cache), so the number
   // of outstanding loads is static and the waits stay counted instead of vmcnt(0)
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    if constexpr (ST) load_words<W, true>(row + b.off, b.row[j]);
-    else load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
+    load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
   }
   if (VN) {
     load_row<W, IBL_NT>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
@@ -253,13 +226,7 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   }
   // the output-edge targets travel in the same in-order vector-memory stream as the rows, one
   // lane per edge (a scalar load would make the LDS waits conservative); v_readlane at the store
-  // fold passes (MAXD <= 8): lanes 8 + j / 16 + j carry fold_other / fold_var of edge j in the same register
-  // (vector loads: a scalar load inside the node body would wait with lgkmcnt(0), i.e. for every LDS
-  // lookup in flight)
-  if constexpr (FOLD)
-    b.tgv = (uint32_t)(lane < 8 ? a.tgt : lane < 16 ? a.fold_other : a.fold_var)[b.st + min(lane & 7, b.d - 1)];
-  else
-    b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
+  b.tgv = (uint32_t)a.tgt[b.st + min(lane, b.d - 1)];
 }
 
 // Empty asm that consumes every register of a fetched item: the compiler inserts ONE counted
@@ -310,50 +277,15 @@ __device__ __forceinline__ void col_bases(const int8_t (&cc)[4], uint32_t lane8c
   for (int i = 0; i < 4; ++i) cb[i] = lane8c + ((uint32_t)cc[i] << 12);
 }
 
-// Degree-2 variable fold of one output word o (8 codewords): the variable's extrinsic output towards its
-// other check is table[ch][o] (vn_group<2>: one lookup per codeword in the final, matching-composed
-// degree-2 table), ch = its channel word.
-__device__ __forceinline__ uint32_t fold_word(uint32_t lane4, uint32_t ch, uint32_t o, uint32_t fbase) {
-  uint32_t t[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[k] = luc(nib(ch, k), qidx(nib(o, k), lane4), fbase);
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r |= t[k] << (4 * k);
-  return r;
-}
-
-
-template <int D, bool GATHER, bool FOLD, class Buf>
+template <int D, bool GATHER, class Buf>
 __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, const Buf& b,
                                            int fslot, bool do_par, bool& unsat) {
   constexpr int W = Buf::W;
-  constexpr bool ST = IBL_CN_STRIDED;
-  // degree-2 fold (IbFastArgs::fold_mode): up to two edge positions p0 < p1 (b.fm) whose variable has
-  // degree 2; their output is run through that variable's final table with its channel word and written to
-  // the variable's other check row of the next check inbox (fold_word). Pass 0 gathered those channel rows
-  // as its inputs already; later passes load them here.
-  const int fm = FOLD ? b.fm : 0;
-  const int p0 = fm ? __builtin_ctz(fm) : 0;
-  const int p1 = (fm & (fm - 1)) ? __builtin_ctz(fm & (fm - 1)) : p0;
-  // row bases stay wave-uniform (SGPRs); the lane's byte offset is added at each access (saddr + voffset)
-  const uint8_t* fch0 = FOLD && !ST ? a.ch8 + (size_t)__builtin_amdgcn_readlane(b.tgv, 16 + p0) * a.ldb : nullptr;
-  const uint8_t* fch1 = FOLD && !ST ? a.ch8 + (size_t)__builtin_amdgcn_readlane(b.tgv, 16 + p1) * a.ldb : nullptr;
-  uint32_t fch[2][W];
-  if constexpr (FOLD && !GATHER && !ST) {
-    if (fm && !IBL_FOLD_LATE) {
-      load_row<W>(fch0 + b.off, fch[0]);
-      load_row<W>(fch1 + b.off, fch[1]);
-    }
-  }
-  uint32_t outw[ST ? 1 : D][W], trow[D], cb[4];
+  uint32_t outw[D][W], trow[D], cb[4];
   col_bases(a.ccol[D], lane8c, cb);
-  if constexpr (!ST) {
 #pragma unroll
-    for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
-  }
+  for (int w = 0; w < D; ++w) trow[w] = __builtin_amdgcn_readlane(b.tgv, w);
   const uint32_t fbase = slot_off(fslot);
-  const uint32_t ffb = FOLD ? slot_off(a.fold_slot) : 0;
   if (do_par) {
     // Syndrome of all 8 codewords of a word at once (calc_syndrome, kernels_template_irreg.cl:
     // 304-326: parity of (m < T/2) over the check's inputs). Adding 8 - T/2 to every nibble sets
@@ -369,25 +301,13 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
       uint32_t x = (D & 1) ? 0x88888888u : 0u;
 #pragma unroll
       for (int j = 0; j < D; ++j) x ^= b.row[j][i] + bias;
-      any |= x & 0x88888888u & valid_nib8(a.B - b.cwb - (ST ? 512 : 8) * i);
+      any |= x & 0x88888888u & valid_nib8(a.B - b.cwb - 8 * i);
     }
     if (__ballot(any != 0) != 0ull) unsat = true;
   }
 #pragma unroll
   for (int i = 0; i < W; ++i) {
-    uint32_t in[D], o[D], fc[2];
-    if constexpr (FOLD && !GATHER && ST) {
-      // this word's fold channel words, requested before its lookups (row bases read out of the lanes
-      // here, so they do not occupy SGPRs across the word)
-      if (fm) {
-        uint32_t tv = b.tgv;
-        asm volatile("" : "+v"(tv));
-        const uint8_t* c0 = a.ch8 + (size_t)__builtin_amdgcn_readlane(tv, 16 + p0) * a.ldb;
-        const uint8_t* c1 = a.ch8 + (size_t)__builtin_amdgcn_readlane(tv, 16 + p1) * a.ldb;
-        fc[0] = *reinterpret_cast<const uint32_t*>(c0 + (b.off + 256u * i));
-        fc[1] = *reinterpret_cast<const uint32_t*>(c1 + (b.off + 256u * i));
-      }
-    }
+    uint32_t in[D], o[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       in[j] = b.row[j][i];
@@ -413,55 +333,11 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
     } else {
       cn_word<D>(lane4, in, fbase, cb, o);
     }
-    if constexpr (ST) {
-      const uint32_t wo = b.off + 256u * i;
-      // target rows read out of the lanes at each word's stores (an opaque copy per word keeps the
-      // compiler from holding D row bases in SGPRs across the next word's lookups)
-      uint32_t tv = b.tgv;
-      asm volatile("" : "+v"(tv));
 #pragma unroll
-      for (int w = 0; w < D; ++w) {
-        const uint32_t tr = __builtin_amdgcn_readlane(tv, w);
-        if (FOLD && ((fm >> w) & 1)) {
-          const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fc[0] : fc[1]);
-          store_word(a.fold_out + (size_t)__builtin_amdgcn_readlane(tv, 8 + w) * (uint32_t)a.ldb + wo,
-                     fold_word(lane4, ch, o[w], ffb));
-          if (a.fold_mode == 2) store_word(a.out + (size_t)tr * (uint32_t)a.ldb + wo, o[w]);
-        } else {
-          store_word(a.out + (size_t)tr * (uint32_t)a.ldb + wo, o[w]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int w = 0; w < D; ++w) outw[ST ? 0 : w][i] = o[w];
-    }
+    for (int w = 0; w < D; ++w) outw[w][i] = o[w];
   }
-  if constexpr (!ST) {
-    if (FOLD && fm) {
-      if constexpr (!GATHER && IBL_FOLD_LATE) {
-        load_row<W>(fch0 + b.off, fch[0]);
-        load_row<W>(fch1 + b.off, fch[1]);
-      }
 #pragma unroll
-      for (int w = 0; w < D; ++w) {
-        if (!((fm >> w) & 1)) {
-          store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
-          continue;
-        }
-        uint32_t f[W];
-#pragma unroll
-        for (int i = 0; i < W; ++i) {
-          const uint32_t ch = GATHER ? b.row[w][i] : (w == p0 ? fch[0][i] : fch[1][i]);
-          f[i] = fold_word(lane4, ch, outw[w][i], ffb);
-        }
-        store_row<W>(a.fold_out + (size_t)__builtin_amdgcn_readlane(b.tgv, 8 + w) * (uint32_t)a.ldb + b.off, f);
-        if (a.fold_mode == 2) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
-      }
-    } else {
-#pragma unroll
-      for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
-    }
-  }
+  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ---------------------------------------------------------------- variable node
@@ -585,7 +461,7 @@ __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
 #ifndef IBL_LIGHT_DEPTH
 #define IBL_LIGHT_DEPTH 2
 #endif
-template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2, bool FOLD = false>
+template <class Buf, bool VN, bool GATHER, int DLO, int DEPTH = 2>
 __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int first,
                                          int end, int nw, int wpb, int* ctr, bool do_par, bool& unsat,
                                          uint64_t* trace_items, const PhaseItems pi) {
@@ -602,7 +478,7 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
       }
     } else {
       switch (cur.d) {
-#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D, GATHER, FOLD>(a, lane4, lane8c, cur, a.fslot[D], do_par, unsat); break;
+#define X(D) case D: if constexpr (D > DLO && D <= Buf::kMax) cn_compute<D, GATHER>(a, lane4, lane8c, cur, a.fslot[D], do_par, unsat); break;
         IBL_DEG_CASES(X)
 #undef X
         default: break;
@@ -626,25 +502,25 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb, Cc;
     int ia = item_of(take_ticket(ctr, lane));
     if (ia >= end) return;
-    fetch_item<Buf, VN, GATHER, FOLD>(a, ia, lane, A, pi);
+    fetch_item<Buf, VN, GATHER>(a, ia, lane, A, pi);
     int ib = item_of(take_ticket(ctr, lane));
-    fetch_item<Buf, VN, GATHER, FOLD>(a, min(ib, end - 1), lane, Bb, pi);
+    fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int ic = item_of(kn);
-      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ic, end - 1), lane, Cc, pi);
+      fetch_item<Buf, VN, GATHER>(a, min(ic, end - 1), lane, Cc, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (ib >= end) break;
       ia = item_of(kn);
-      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ia, end - 1), lane, A, pi);
+      fetch_item<Buf, VN, GATHER>(a, min(ia, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
       if (ic >= end) break;
       ib = item_of(kn);
-      fetch_item<Buf, VN, GATHER, FOLD>(a, min(ib, end - 1), lane, Bb, pi);
+      fetch_item<Buf, VN, GATHER>(a, min(ib, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(Cc);
       ++done;
@@ -654,18 +530,18 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
     Buf A, Bb;
     int item = item_of(take_ticket(ctr, lane));
     if (item >= end) return;
-    fetch_item<Buf, VN, GATHER, FOLD>(a, item, lane, A, pi);
+    fetch_item<Buf, VN, GATHER>(a, item, lane, A, pi);
     int kn = take_ticket(ctr, lane);
     for (;;) {
       int next = item_of(kn);
-      fetch_item<Buf, VN, GATHER, FOLD>(a, min(next, end - 1), lane, Bb, pi);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, Bb, pi);
       kn = take_ticket(ctr, lane);
       compute(A);
       ++done;
       if (next >= end) break;
       item = next;
       next = item_of(kn);
-      fetch_item<Buf, VN, GATHER, FOLD>(a, min(next, end - 1), lane, A, pi);
+      fetch_item<Buf, VN, GATHER>(a, min(next, end - 1), lane, A, pi);
       kn = take_ticket(ctr, lane);
       compute(Bb);
       ++done;
@@ -677,7 +553,7 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
   if (trace_items && lane == 0) *trace_items += (uint64_t)done;
 }
 
-template <int MAXD, bool VN, bool GATHER, bool FOLD = false>
+template <int MAXD, bool VN, bool GATHER>
 __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;  // LDS address = byte offset (base checked 0)
@@ -709,10 +585,10 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #pragma unroll 1
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)
-      ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD, 2, FOLD>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
+      ib_phase<ItemBuf<MAXD, W>, VN, GATHER, kLightD, 2>(a, lane4, lane8c, lane, 0, heavy_end, nw, wpb, ctr, do_par, unsat,
                                                       trace_items, PhaseItems{0, 0, a.nchunks});
     else
-      ib_phase<ItemBuf<kLightD, LW>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2), FOLD>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
+      ib_phase<ItemBuf<kLightD, LW>, VN, GATHER, 0, (VN ? IBL_LIGHT_DEPTH : 2)>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr + 1, do_par,
                                                    unsat, trace_items, PhaseItems{heavy_end, a.n_heavy, nch_l});
   }
   if (a.trace && lane == 0) {
@@ -735,30 +611,21 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #ifndef IBL_WPE8
 #define IBL_WPE8 1
 #endif
-// FOLD: the degree-2 variable fold (IbFastArgs::fold_mode != 0; MAXD=8 codes only) is its own
-// instantiation, so codes without it keep the plain body's registers
-#ifndef IBL_LB8F
-#define IBL_LB8F 768
-#endif
-template <int MAXD, bool GATHER, bool FOLD = false>
-// check-pass bounds of their own (default: the shared ones): IBL_LB8C / IBL_WPE8C (MAXD=8), IBL_WPE8F (fold)
+// check-pass bounds of their own (default: the shared ones): IBL_LB8C / IBL_WPE8C (MAXD=8)
 #ifndef IBL_LB8C
 #define IBL_LB8C IBL_LB8
 #endif
 #ifndef IBL_WPE8C
 #define IBL_WPE8C IBL_WPE8
 #endif
-#ifndef IBL_WPE8F
-#define IBL_WPE8F IBL_WPE8
-#endif
-__global__ __launch_bounds__(MAXD <= 8 ? (FOLD ? IBL_LB8F : IBL_LB8C) : IBL_LB16,
-                             MAXD <= 8 ? (FOLD ? IBL_WPE8F : IBL_WPE8C) : 1) void ib_cn_fast(IbFastArgs a) {
+template <int MAXD, bool GATHER>
+__global__ __launch_bounds__(MAXD <= 8 ? IBL_LB8C : IBL_LB16, MAXD <= 8 ? IBL_WPE8C : 1) void ib_cn_fast(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   if (!gate_open(a.gate, threadIdx.x & 63)) return;  // every wave reads the same words: uniform exit
   lds_at_zero(lds);
   stage_pass(lds, a);
   __syncthreads();
-  ib_pass<MAXD, false, GATHER, FOLD>(a, lds);
+  ib_pass<MAXD, false, GATHER>(a, lds);
 }
 
 template <int MAXD>
@@ -1471,12 +1338,10 @@ hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch
 }
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
   if (a.gather) {
-    if (maxd <= 8 && a.fold_mode) hipLaunchKernelGGL((ib_cn_fast<8, true, true>), dim3(grid), dim3(block), lds, s, a);
-    else if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, true>), dim3(grid), dim3(block), lds, s, a);
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, true>), dim3(grid), dim3(block), lds, s, a);
     else hipLaunchKernelGGL((ib_cn_fast<16, true>), dim3(grid), dim3(block), lds, s, a);
   } else {
-    if (maxd <= 8 && a.fold_mode) hipLaunchKernelGGL((ib_cn_fast<8, false, true>), dim3(grid), dim3(block), lds, s, a);
-    else if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, false>), dim3(grid), dim3(block), lds, s, a);
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_fast<8, false>), dim3(grid), dim3(block), lds, s, a);
     else hipLaunchKernelGGL((ib_cn_fast<16, false>), dim3(grid), dim3(block), lds, s, a);
   }
   return hipGetLastError();
@@ -1492,15 +1357,13 @@ hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t ld
   return hipGetLastError();
 }
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu) {
-  if (which == 0 || which == 3) {  // every variant must accept the LDS size; report the non-gather one
-    for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>,
-                          (const void*)ib_cn_fast<8, true, true>, (const void*)ib_cn_fast<8, false, true>}) {
+  if (which == 0) {  // every variant must accept the LDS size; report the non-gather one
+    for (const void* g : {(const void*)ib_cn_fast<8, true>, (const void*)ib_cn_fast<16, true>}) {
       hipError_t e = hipFuncSetAttribute(g, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
       if (e != hipSuccess) return e;
     }
   }
-  const void* f = which == 3 ? (const void*)ib_cn_fast<8, false, true>   // degree-2 fold variant (MAXD=8)
-                : which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
+  const void* f = which == 0 ? (maxd <= 8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>)
                 : which == 1 ? (maxd <= 8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>)
                              : (const void*)ib_dec_fast;
   hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
@@ -1511,19 +1374,16 @@ hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* bl
   if (block > fa.maxThreadsPerBlock) return hipErrorInvalidValue;  // above the kernel's launch bounds
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, block, lds);
 }
-hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, bool fold, size_t* bytes, const char** name) {
+hipError_t ib_fast_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
   const bool c8 = cn_maxd <= 8, v8 = vn_maxd <= 8;
   const struct { const void* f; const char* n; } ks[] = {
       {c8 ? (const void*)ib_cn_fast<8, true> : (const void*)ib_cn_fast<16, true>, c8 ? "ib_cn_fast<8,gather>" : "ib_cn_fast<16,gather>"},
       {c8 ? (const void*)ib_cn_fast<8, false> : (const void*)ib_cn_fast<16, false>, c8 ? "ib_cn_fast<8>" : "ib_cn_fast<16>"},
       {v8 ? (const void*)ib_vn_fast<8> : (const void*)ib_vn_fast<16>, v8 ? "ib_vn_fast<8>" : "ib_vn_fast<16>"},
-      {(const void*)ib_dec_fast, "ib_dec_fast"},
-      {fold ? (const void*)ib_cn_fast<8, true, true> : nullptr, "ib_cn_fast<8,gather,fold>"},
-      {fold ? (const void*)ib_cn_fast<8, false, true> : nullptr, "ib_cn_fast<8,fold>"}};
+      {(const void*)ib_dec_fast, "ib_dec_fast"}};
   *bytes = 0;
   *name = "";
   for (const auto& k : ks) {
-    if (!k.f) continue;
     hipFuncAttributes fa;
     const hipError_t e = hipFuncGetAttributes(&fa, k.f);
     if (e != hipSuccess) return e;

@@ -113,12 +113,12 @@ class IBDecoder:
         _lib.check(_lib.load().ibl_ib_path_in_use(self._h, ctypes.byref(f)), "ibl_ib_path_in_use")
         return bool(f.value)
 
-    @property
-    def fold(self) -> bool:
-        """The per-pass path folds the degree-2 variables into the check pass (``ibl_ib_features``)."""
-        f = ctypes.c_int32()
-        _lib.check(_lib.load().ibl_ib_features(self._h, ctypes.byref(f)), "ibl_ib_features")
-        return bool(f.value & _lib.IBL_FEAT_FOLD)
+    def fused_ncw(self, B: int) -> int:
+        """Codewords per workgroup the fused kernel decodes a batch of ``B`` with (8, or 4 for half
+        groups; 0 when the fused kernel is not in use) — ``ibl_ib_fused_ncw``."""
+        n = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_ib_fused_ncw(self._h, int(B), ctypes.byref(n)), "ibl_ib_fused_ncw")
+        return int(n.value)
 
     def decode(self, ch: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=torch.int32,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:

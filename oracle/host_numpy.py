@@ -22,8 +22,13 @@ stop, no matching — the host path has none):
 
 Each pass is the reference's numpy shape of work: a gather of every node's inbox rows
 (``all_messages``), a gather of the d(d-1) "others" entries (``reduced``), the d-1 (or d-2) chained
-table lookups on the whole [rows] vector, and a scatter to the other inbox. The "others" index pattern
-(built in the reference from ``np.kron`` / ``np.eye`` masks every pass) is built once per degree.
+table lookups on the whole [rows] vector, and a scatter to the other inbox. By default the "others"
+index pattern (built in the reference from ``np.kron`` / ``np.eye`` masks every pass) is built once per
+degree and the inboxes are flat vectors (shape-optimised); ``faithful_shape=True`` keeps the
+reference's shape of work as well: the masks rebuilt with ``np.kron`` / ``np.eye`` in every pass
+(``discrete_LDPC_decoder.py:376-378,385-388``, ``discrete_LDPC_decoder_irreg.py:462-465,482-485,498-501``),
+the channel matrix built with ``np.kron`` (:361), and [E][1] inboxes addressed through column 0. Both
+give identical outputs; the bench reports both per-core rates.
 Pinned: equal, bit for bit, to the reference's own outputs in ``tests/golden/reference_host.npz``
 (``tests/test_cpu_oracle.py``).
 """
@@ -39,12 +44,20 @@ def _others(d: int) -> np.ndarray:
     return np.array([j for w in range(d) for j in range(d) if j != w], dtype=np.int64)
 
 
+def _others_kron(d: int) -> np.ndarray:
+    """The same pattern the way the reference builds it in every pass: kron of the index column with a
+    row of ones, transposed, masked by the off-diagonal of eye(d)."""
+    m = np.kron(np.arange(d)[:, np.newaxis], np.ones(d))
+    return m.transpose()[(1 - np.eye(d)).astype(bool)].astype(int)
+
+
 class HostDecoder:
     """decode_on_host for one code and one table set. ``regular`` selects the regular class's
     schedule and table offsets (degrees from the first node, as ``degree_*_nr[0]`` there)."""
 
-    def __init__(self, g, Tc: int, T: int, imax: int, cn_lut, vn_lut, regular: bool):
+    def __init__(self, g, Tc: int, T: int, imax: int, cn_lut, vn_lut, regular: bool, faithful_shape: bool = False):
         self.g, self.Tc, self.T, self.imax, self.regular = g, int(Tc), int(T), int(imax), bool(regular)
+        self.faithful = bool(faithful_shape)
         self.cn_lut = np.asarray(cn_lut, dtype=np.int64)
         self.vn_lut = np.asarray(vn_lut, dtype=np.int64)
         cdeg, vdeg = np.asarray(g.cn_deg), np.asarray(g.vn_deg)
@@ -91,12 +104,21 @@ class HostDecoder:
 
     def _check_pass(self, cin: np.ndarray, vin: np.ndarray, it: int) -> None:
         for d, rows, oth, tgt in self.checks:
+            if self.faithful:                                  # [E][1] inboxes, masks rebuilt every pass
+                red = cin[rows][:, _others_kron(d)].reshape(-1, d - 1)
+                vin[tgt, 0] = self._cn_op(red, it)
+                continue
             allm = cin[rows]                                   # all_messages
             red = allm[:, oth].reshape(-1, d - 1)              # reduced: one row per output edge
             vin[tgt] = self._cn_op(red, it)
 
     def _var_pass(self, ch: np.ndarray, vin: np.ndarray, cin: np.ndarray, it: int) -> None:
         for d, sel, rows, oth, tgt in self.vars:
+            if self.faithful:
+                chm = np.kron(ch[sel][:, np.newaxis], np.ones((d, 1))).astype(int)
+                red = vin[rows][:, _others_kron(d)].reshape(-1, d - 1)
+                cin[:, 0][tgt] = self._vn_op(np.hstack((chm, red)), it)
+                continue
             chm = np.repeat(ch[sel], d)[:, None]               # channel_val_mat (np.kron of the column)
             red = vin[rows][:, oth].reshape(-1, d - 1)
             cin[tgt] = self._vn_op(np.hstack((chm, red)), it)
@@ -105,10 +127,14 @@ class HostDecoder:
         """One codeword: [N] channel cluster ids -> [N] decided cluster ids (int64)."""
         g = self.g
         ch = np.asarray(channel_values).astype(np.int64).reshape(-1)
-        cin = np.zeros(g.n_e, dtype=np.int64)
-        vin = np.zeros(g.n_e, dtype=np.int64)
+        shape = (g.n_e, 1) if self.faithful else (g.n_e,)
+        cin = np.zeros(shape, dtype=np.int64)
+        vin = np.zeros(shape, dtype=np.int64)
         for d, sel, rows, _, tgt in self.vars:                 # send the channel values
-            cin[tgt] = np.repeat(ch[sel], d)
+            if self.faithful:
+                cin[:, 0][tgt] = np.kron(ch[sel][:, np.newaxis], np.ones((d, 1))).astype(int).reshape(-1)
+            else:
+                cin[tgt] = np.repeat(ch[sel], d)
         if self.regular:
             for it in range(self.imax):
                 self._check_pass(cin, vin, it)
@@ -120,5 +146,6 @@ class HostDecoder:
                 self._check_pass(cin, vin, it + 1)
         out = np.zeros(g.n_v, dtype=np.int64)
         for d, sel, rows, _, _ in self.vars:                   # decision over all inputs
-            out[sel] = self._vn_op(np.hstack((ch[sel][:, None], vin[rows])), self.imax - 1)
+            allm = vin[rows][:, :, 0] if self.faithful else vin[rows]
+            out[sel] = self._vn_op(np.hstack((ch[sel][:, None], allm)), self.imax - 1)
         return out

@@ -9,8 +9,9 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from informationbottleneckdecodingldpc_amd import tables, tables_io
+from informationbottleneckdecodingldpc_amd import engine, tables, tables_io
 from informationbottleneckdecodingldpc_amd.awgn_quantizer import AWGN_Channel_Quantizer
+from informationbottleneckdecodingldpc_amd import ber
 from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
 from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
 from oracle import oracle
@@ -167,20 +168,67 @@ def _free_port():
     return p
 
 
+class _GlobalQuanti(_FakeQuanti):
+    """Hands the decoder the global batch index its Philox offset encodes."""
+    def quantize_direct_OpenCL(self, N, B, dtype=None):
+        return (self.sigma_n2, self.offset // engine.philox_blocks(N, B))
+
+
+class _GlobalIB(_FakeIB):
+    """Errors of a batch = a scripted function of (Eb/N0, global batch index): any rank that decodes
+    global batch g reports the same count, so equal sweeps prove equal frames."""
+    def decode_OpenCL(self, rec, buffer_in=False, return_buffer=False):
+        return rec
+
+    def return_errors_all_zero(self, rec):
+        s2, g = rec
+        ebn0 = -10 * np.log10(s2 * 2 * 0.5)
+        return float(((g * 7919) % 13) * self.B * 10 ** (-ebn0))
+
+
+_SWEEP = dict(EbN0_dB_start=0.0, EbN0_dB_max_value=1.0, EbN0_dB_normal_stepwidth=0.5, EbN0_dB_small_stepwidth=0.25,
+              target_error_rate=1e-12, msg_at_time=10, min_errors=300, max_blocks=170)
+
+
+def test_global_batch_offsets():
+    # world 3: rank r's round j is global batch base + 3 j + r; every index exactly once
+    seen = sorted(ber.global_batch(5, j, r, 3) for j in range(4) for r in range(3))
+    assert seen == list(range(5, 17))
+    assert ber.global_batch(0, 2, 1, 2) == 5
+
+
+@pytest.mark.parametrize("world,sync", [(2, 1), (3, 1), (2, 3), (4, 2)])
+def test_ber_sweep_is_world_size_invariant(world, sync):
+    """Emulated k-rank sweeps (lockstep, in-memory exchange) count exactly the frames of the 1-rank sweep:
+    same points, error and block counts, although the stop falls inside a round (min_errors) or at
+    max_blocks (170 = 17 batches, not a multiple of world * sync_every)."""
+    one = run_ber(_GlobalIB(None), BERConfig(**_SWEEP), quantizer_factory=_GlobalQuanti)
+    many = ber.run_ber_lockstep(_GlobalIB(None), BERConfig(**_SWEEP, sync_every=sync), world,
+                                quantizer_factory=_GlobalQuanti)
+    assert len(one.errors) == 3 and one.blocks[-1] == 170 and one.blocks[0] < 170
+    assert many.errors == one.errors and many.blocks == one.blocks
+    np.testing.assert_array_equal(many.BER_vector, one.BER_vector)
+    np.testing.assert_array_equal(many.EbN0_dB_vector, one.EbN0_dB_vector)
+
+
+def test_ber_world_override_needs_process_group():
+    with pytest.raises(ValueError, match="run_ber_lockstep"):
+        run_ber(_GlobalIB(None), BERConfig(**_SWEEP), quantizer_factory=_GlobalQuanti, world=2)
+
+
 def _ber_worker(rank, port, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
-        # rank 1 sees twice the errors: the summed counter must drive both ranks identically
-        cfg = BERConfig(EbN0_dB_start=0.0, EbN0_dB_max_value=0.0, min_errors=90, msg_at_time=10, sync_every=2)
-        r = run_ber(_FakeIB(lambda s2: 1.0 * (rank + 1)), cfg, quantizer_factory=_FakeQuanti)
+        r = run_ber(_GlobalIB(None), BERConfig(**_SWEEP, sync_every=2), quantizer_factory=_GlobalQuanti)
         q.put((rank, list(r.errors), list(r.blocks)))
     finally:
         dist.destroy_process_group()
 
 
 def test_ber_counters_reduce_over_gloo_ranks():
+    """Two processes over gloo (the all-reduce exchange) give the 1-rank sweep's counts on both ranks."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -191,6 +239,6 @@ def test_ber_counters_reduce_over_gloo_ranks():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
+    one = run_ber(_GlobalIB(None), BERConfig(**_SWEEP), quantizer_factory=_GlobalQuanti)
     (r0, e0, b0), (r1, e1, b1) = res
-    # per sync (2 batches per rank): 2*10*1 + 2*10*2 = 60 errors, 40 blocks -> stops after 2 syncs
-    assert e0 == e1 == [120] and b0 == b1 == [80]
+    assert e0 == e1 == one.errors and b0 == b1 == one.blocks

@@ -197,3 +197,30 @@ def test_generated_schedules_are_current():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_sched.py"), *args],
                        capture_output=True, text=True, check=True)
     assert r.stdout == text
+
+
+def test_device_graph_lives_with_its_decoder(monkeypatch, wlan_H):
+    """the device copy of a decoder's edge arrays is held by the decoder, not by a module
+    cache, so 100 decoders constructed and dropped (one per Eb/N0 point, say) leave no device graph alive."""
+    import gc
+    import weakref
+
+    import torch
+    from informationbottleneckdecodingldpc_amd import _dropin
+
+    class FakeGraph:
+        def __init__(self, edges, dev):
+            self.edges = edges
+
+    monkeypatch.setattr(_dropin, "Graph", FakeGraph)
+    refs = []
+    for _ in range(100):
+        d = _dropin.CodeMixin()
+        d._init_code(wlan_H)
+        g = d._graph_on(torch.device("cuda", 0))
+        assert d._graph_on(torch.device("cuda", 0)) is g          # reused per decoder and device
+        refs.append(weakref.ref(g))
+        del d, g
+    gc.collect()
+    assert not hasattr(_dropin, "_GRAPH_CACHE")
+    assert sum(r() is not None for r in refs) == 0

@@ -106,15 +106,18 @@ def test_llr_tables_decode_on_oracle(wlan_H):
     assert (out[:g.data_len] < 8).sum() == 0
 
 
+@pytest.mark.parametrize("faithful", [False, True])
 @pytest.mark.parametrize("name", ["reg", "wlan"])
 @pytest.mark.parametrize("imax", [1, 2, 10])
-def test_numpy_host_decoder_equals_reference_decode_on_host(golden, reg_H, wlan_H, name, imax):
-    """oracle/host_numpy.py (the C1 CPU baseline: decode_on_host restated in numpy) == the reference's
-    own decode_on_host outputs, regular and irregular class, codeword by codeword."""
+def test_numpy_host_decoder_equals_reference_decode_on_host(golden, reg_H, wlan_H, name, imax, faithful):
+    """oracle/host_numpy.py (the C1 CPU baseline: decode_on_host restated in numpy, shape-optimised and in
+    the reference's own shape of work) == the reference's own decode_on_host outputs, regular and
+    irregular class, codeword by codeword."""
     from oracle.host_numpy import HostDecoder
     g = graph.build_graph(reg_H if name == "reg" else wlan_H)
     z = golden
-    dec = HostDecoder(g, 16, 16, imax, z[f"{name}_imax{imax}_cn"], z[f"{name}_imax{imax}_vn"], regular=(name == "reg"))
+    dec = HostDecoder(g, 16, 16, imax, z[f"{name}_imax{imax}_cn"], z[f"{name}_imax{imax}_vn"], regular=(name == "reg"),
+                      faithful_shape=faithful)
     ch = z[f"{name}_imax{imax}_ch"]
     for k in range(ch.shape[1]):
         np.testing.assert_array_equal(dec.decode(ch[:, k]), z[f"{name}_imax{imax}_out"][:, k])

@@ -146,3 +146,31 @@ def test_minsum_fp32_ber_curve_equals_oracle():
         return oracle.float32_decode(g, 30, llr, early_stop=True)
     ref = _replay(cfg, g.n_v, dec.data_len, float(dec.R_c), decode, lambda out, dl: float((out[:dl] < 0).sum()))
     _assert_same(r, ref)
+
+
+def test_bp_c5_sweep_world_size_invariant(dvb_H):
+    """C5's BP sweep (DVB-S2, i_max=100, fp64, B=8) as an emulated 2-rank run (``run_ber_lockstep``: rank 0
+    and rank 1 decode global batches 2j and 2j+1, counters exchanged per round) and as a 3-rank run with
+    two rounds per exchange equals the 1-rank sweep and the oracle replay point for point. min_errors
+    stops the first points inside a round (the extra batches are discarded), max_blocks = 5 batches the
+    later ones — neither is a multiple of the world size (``ber._rank_sweep``)."""
+    from informationbottleneckdecodingldpc_amd.ber import run_ber_lockstep
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    g = graph.build_graph(dvb_H)
+    B, imax = 8, 100
+    bp = BeliefPropagationDecoderClassIrregular(dvb_H, imax, 16, B, precision=torch.float64)
+    cfg = BERConfig(EbN0_dB_start=0.2, EbN0_dB_max_value=1.2, EbN0_dB_normal_stepwidth=0.4,
+                    EbN0_dB_small_stepwidth=0.2, target_error_rate=1e-9, min_errors=20000, msg_at_time=B,
+                    max_blocks=40, seed=31, llr_dtype=torch.float64)
+    one = run_ber(bp, cfg)
+    two = run_ber_lockstep(bp, cfg, 2)
+    cfg3 = BERConfig(**{**cfg.__dict__, "sync_every": 2})
+    three = run_ber_lockstep(bp, cfg3, 3)
+
+    def decode(cl, q):
+        return oracle.float_decode(g, oracle.BP, imax, q.output_LLRs[cl], early_stop=True)
+    ref = _replay(cfg, g.n_v, bp.data_len, float(bp.R_c), decode, lambda out, dl: float((out[:dl] < 0).sum()))
+    print(f"C5 world-invariance: points {list(ref[0])} errors {ref[2]} blocks {ref[3]}")
+    for r in (one, two, three):
+        _assert_same(r, ref)
+    assert ref[3][0] < cfg.max_blocks and ref[3][-1] == cfg.max_blocks   # both stop rules exercised

@@ -32,19 +32,8 @@ VARIANTS = {
     "lw4d2": ["IBL_LIGHT_W=4", "IBL_LIGHT_DEPTH=2"],
     # plain (cached) variable-pass row accesses instead of the default nontemporal ones
     "nt0": ["IBL_NT=0"],
-    # degree-2 fold check kernel at 1024-thread launch bounds (spills: run with IBL_ALLOW_SCRATCH=1)
-    "f1024": ["IBL_LB8F=1024"],
-    # check-pass strided word layout (lane l's word i = dword 64 i + l; outputs stored per word), and the
-    # same with the fold kernel at 1024-thread launch bounds
-    "cst": ["IBL_CN_STRIDED=1"],
-    "cstf": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024"],
-    # check schedule of 2 codewords x 4 chains (half the column-term registers of 4 x 2): alone, with the
-    # strided layout, with the fold kernel at 1024 threads, and with 5 check waves per SIMD (256-thread blocks)
+    # check schedule of 2 codewords x 4 chains (half the column-term registers of 4 x 2)
     "s2n": ['IBL_SCHED_FILE="ib_sched_s2n.inc"'],
-    "cs2": ["IBL_CN_STRIDED=1", 'IBL_SCHED_FILE="ib_sched_cs2.inc"'],
-    "cs2f": ["IBL_CN_STRIDED=1", "IBL_LB8F=1024", 'IBL_SCHED_FILE="ib_sched_cs2f.inc"'],
-    "cs2o5": ["IBL_CN_STRIDED=1", "IBL_LB8C=256", "IBL_WPE8C=5", "IBL_LB8F=1024",
-              'IBL_SCHED_FILE="ib_sched_cs2o5.inc"'],
     # one dword per lane (8 codewords) and all 8 in one check-schedule group: 16 check chains in flight
     "w1s8": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1s8.inc"'],
     "w1l4": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1l4.inc"'],
@@ -59,10 +48,14 @@ VARIANTS = {
     "nc22": ["IBL_NC_CN=2", "IBL_NC_VN=2", 'IBL_SCHED_FILE="ib_sched_nc22.inc"'],
     "nc33": ["IBL_NC_CN=3", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc33.inc"'],
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
+    # float kernels with the IEEE mode bit on and NaNs honoured (the round-2 float build flags)
+    "ieee": [],
 }
+# per-source flag overrides (replace _build.SRC_FLAGS)
+SRC_FLAGS = {"ieee": {}}
 # gen_sched.py arguments of the variants that need their own schedule file
 SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3",
-              "s2n": "2 4 2 4 0 0", "cs2": "2 4 2 4 0 0", "cs2f": "2 4 2 4 0 0", "cs2o5": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0"}
+              "s2n": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0"}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
@@ -75,5 +68,5 @@ if __name__ == "__main__":
                 subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "gen_sched.py"),
                                 *SCHED_ARGS[n].split()], stdout=f, check=True)
         lib = os.path.join(outdir, f"libibldpc_{n}.so")
-        _build.build(defines=VARIANTS[n], lib=lib, tag=n, force="--force" in os.environ.get("VARIANT_FLAGS", ""))
+        _build.build(defines=VARIANTS[n], lib=lib, tag=n, src_flags=SRC_FLAGS.get(n), force="--force" in os.environ.get("VARIANT_FLAGS", ""))
         print(lib)
