@@ -705,6 +705,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
   if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+  if (a.flow && threadIdx.x < 128) reinterpret_cast<int*>(lds + a.done_off)[threadIdx.x] = -1;
   SlotIdx vs{nullptr, a.vn_slot};
   if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
     uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
@@ -723,6 +724,146 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   constexpr int TW = kFlTraceWords;
   uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && lane == 0) ? a.trace : nullptr;
   if (IBL_FUSED_TRACE && tr && wv == 0) tr[0] = __builtin_readcyclecounter();
+  // ---- task bodies (one task = up to 64 same-degree nodes, lane i = node i) ----
+  // send: every variable's channel slot and its edge slots
+  auto send_task = [&](int t, int grp) __attribute__((always_inline)) {
+    const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+    const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+    if (lane < cnt) {
+      // channel staged as [group][variable position] (fl_stage_t): a task reads consecutive slots
+      const VT c = reinterpret_cast<const VT*>(a.ch)[(size_t)grp * a.n_v + pos + lane];
+      chL[pos + lane] = c;
+      for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
+    }
+  };
+  auto cn_task = [&](int t, int valid, bool do_par, bool& unsat) __attribute__((always_inline)) {
+    const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
+    if (lane < cnt) {
+      switch (d) {
+#define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
+        FL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+    }
+  };
+  auto vn_task = [&](int t) __attribute__((always_inline)) {
+    const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+    const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+    if (lane < cnt) {
+      switch (d) {
+        case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+        FL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+    }
+  };
+  // APP output: ch + all inputs of the last CN pass in ascending edge order, unclamped
+  auto out_task = [&](int t, int cw0, int valid) __attribute__((always_inline)) {
+    const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+    const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+    if (lane < cnt) {
+      const int node = a.vn_node[pos + lane];
+      F x[N];
+      {
+        const VT r = chL[pos + lane];
+#pragma unroll
+        for (int s = 0; s < N; ++s) x[s] = V::get(r, s);
+      }
+      if (L > 0)
+        for (int k = 0; k < d; ++k) {
+          const VT r = msg[vs[sf + k * cnt + lane]];
+#pragma unroll
+          for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
+        }
+      const size_t o = (size_t)node * a.B + cw0;
+      if (a.out_dtype == kF32) {
+        float* p = reinterpret_cast<float*>(a.out) + o;
+        if constexpr (N == 4) {
+          if (a.aligned && valid >= 4) {
+            *reinterpret_cast<float4*>(p) = make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
+            return;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < N; ++s)
+          if (s < valid) p[s] = (float)x[s];
+      } else {
+        double* p = reinterpret_cast<double*>(a.out) + o;
+        if constexpr (N == 2) {
+          if (a.aligned && valid >= 2) {
+            *reinterpret_cast<double2*>(p) = make_double2((double)x[0], (double)x[1]);
+            return;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < N; ++s)
+          if (s < valid) p[s] = (double)x[s];
+      }
+    }
+  };
+
+  if (a.flow && L >= 1) {
+    // ---- task dataflow: no phase barriers. One ticket sequence per block walks its groups' phases in
+    // order (send; CN 1; VN 1; ...; CN L; output) and a task waits only for the tasks of the previous
+    // phase that touch its slots: check task c of phase P for the variable tasks in cn_dep[c] to have
+    // finished phase P-1, a variable / output task for the check tasks in vn_dep[v]; a group's send task v
+    // also for output task v of the previous group (same slots and channel slot). Waits only point back
+    // to smaller tickets, so the oldest unfinished ticket can always run. Done stamps: global phase
+    // index (group iteration k * (2L + 1) + local phase), written by lane 0 after the task's LDS stores.
+    int* done_c = reinterpret_cast<int*>(lds + a.done_off);
+    int* done_v = done_c + 64;
+    const int nc = a.n_cn_tasks, nv = a.n_vn_tasks;
+    const int per = 2 * L + 1, tpg = nv + L * (nc + nv);
+    auto wait_for = [&](const int* done, uint64_t mask, int need) __attribute__((always_inline)) {
+      if (mask == 0) return;
+      for (;;) {
+        const int st = __hip_atomic_load(done + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((__ballot(st >= need) & mask) == mask) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    auto publish = [&](int* done, int t, int P) __attribute__((always_inline)) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(done + t, P, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    for (;;) {
+      const int tk = take_ticket(ctr, lane);
+      const int k = tk / tpg, grp = (int)blockIdx.x + k * (int)gridDim.x;
+      if (grp >= a.ngroups) break;
+      const int cw0 = grp * N, valid = a.B - cw0;
+      int r = tk - k * tpg;
+      const int base = k * per;
+      if (r < nv) {                        // send (local phase 0)
+        if (k > 0) wait_for(done_v, (uint64_t)1 << r, base - 1);
+        send_task(r, grp);
+        publish(done_v, r, base);
+        continue;
+      }
+      r -= nv;
+      const int j = r / (nc + nv) + 1, q = r - (j - 1) * (nc + nv);
+      if (q < nc) {                        // CN pass j (local phase 2j - 1)
+        const int P = base + 2 * j - 1;
+        wait_for(done_v, a.cn_dep[q], P - 1);
+        const bool do_par = a.unsat != nullptr;
+        bool unsat = false;
+        cn_task(q, valid, do_par, unsat);
+        if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
+        publish(done_c, q, P);
+      } else {                             // VN pass j (j < L) or the output (j == L), local phase 2j
+        const int v = q - nc, P = base + 2 * j;
+        wait_for(done_c, a.vn_dep[v], P - 1);
+        if (j < L) vn_task(v);
+        else out_task(v, cw0, valid);
+        publish(done_v, v, P);
+      }
+    }
+    return;
+  }
+
+  // ---- phases separated by barriers
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
     if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
@@ -754,91 +895,16 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
     const int cw0 = grp * N;
     const int valid = a.B - cw0;
-    // send: every variable's channel slot and its edge slots
-    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
-      const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
-      const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
-      if (lane < cnt) {
-        // channel staged as [group][variable position] (fl_stage_t): a task reads consecutive slots
-        const VT c = reinterpret_cast<const VT*>(a.ch)[(size_t)grp * a.n_v + pos + lane];
-        chL[pos + lane] = c;
-        for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
-      }
-    });
+    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { send_task(t, grp); });
     for (int j = 1; j <= L; ++j) {
       const bool do_par = a.unsat != nullptr;
       bool unsat = false;
-      phase(a.n_cn_tasks, [&](int t) __attribute__((always_inline)) {
-        const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
-        if (lane < cnt) {
-          switch (d) {
-#define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
-            FL_DEG_CASES(X)
-#undef X
-            default: break;
-          }
-        }
-      });
+      phase(a.n_cn_tasks, [&](int t) __attribute__((always_inline)) { cn_task(t, valid, do_par, unsat); });
       if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
       if (j == L) break;
-      phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
-        const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
-        const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
-        if (lane < cnt) {
-          switch (d) {
-            case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
-#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
-            FL_DEG_CASES(X)
-#undef X
-            default: break;
-          }
-        }
-      });
+      phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { vn_task(t); });
     }
-    // APP output: ch + all inputs of the last CN pass in ascending edge order, unclamped
-    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) {
-      const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
-      const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
-      if (lane < cnt) {
-        const int node = a.vn_node[pos + lane];
-        F x[N];
-        {
-          const VT r = chL[pos + lane];
-#pragma unroll
-          for (int s = 0; s < N; ++s) x[s] = V::get(r, s);
-        }
-        if (L > 0)
-          for (int k = 0; k < d; ++k) {
-            const VT r = msg[vs[sf + k * cnt + lane]];
-#pragma unroll
-            for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
-          }
-        const size_t o = (size_t)node * a.B + cw0;
-        if (a.out_dtype == kF32) {
-          float* p = reinterpret_cast<float*>(a.out) + o;
-          if constexpr (N == 4) {
-            if (a.aligned && valid >= 4) {
-              *reinterpret_cast<float4*>(p) = make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]);
-              return;
-            }
-          }
-#pragma unroll
-          for (int s = 0; s < N; ++s)
-            if (s < valid) p[s] = (float)x[s];
-        } else {
-          double* p = reinterpret_cast<double*>(a.out) + o;
-          if constexpr (N == 2) {
-            if (a.aligned && valid >= 2) {
-              *reinterpret_cast<double2*>(p) = make_double2((double)x[0], (double)x[1]);
-              return;
-            }
-          }
-#pragma unroll
-          for (int s = 0; s < N; ++s)
-            if (s < valid) p[s] = (double)x[s];
-        }
-      }
-    });
+    phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { out_task(t, cw0, valid); });
     tr = nullptr;   // trace the first group only
   }
 }
