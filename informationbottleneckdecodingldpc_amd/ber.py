@@ -98,12 +98,13 @@ def _dist_world():
 def _dist_exchange(rank: int, world: int):
     """Exchange for one process per rank: every rank's per-batch error counts of one round, as a
     [world][k] list, through one all-reduce of a zero-padded float64 vector (integer counts < 2^53 add
-    exactly). RCCL (``nccl``) reduces a device tensor, gloo a host one."""
+    exactly). RCCL (``nccl``) reduces a device tensor, gloo a host one; an initialised group of size 1
+    still runs the all-reduce (a 1-GPU ``nccl`` group exercises the device path)."""
     def exchange(local):
-        if world == 1:
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
             return [list(local)]
         import torch
-        import torch.distributed as dist
         k = len(local)
         dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
         t = torch.zeros(world * k, dtype=torch.float64, device=dev)

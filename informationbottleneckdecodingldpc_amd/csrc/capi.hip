@@ -689,6 +689,17 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     vn.info = g->vn_info; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
     cn.n_heavy = g->cn_heavy; vn.n_heavy = g->vn_heavy;
+    // diagnostics (timing only, outputs are not decodes): IBL_VN_PART=heavy / light runs the variable
+    // pass over one item class only (the degree > kLightD items, or the rest)
+    if (const char* vp = getenv("IBL_VN_PART")) {
+      if (vp[0] == 'h') {
+        vn.n_nodes = g->vn_heavy;
+      } else if (vp[0] == 'l') {
+        vn.info = g->vn_info + 4 * (size_t)g->vn_heavy;
+        vn.n_nodes = g->n_v - g->vn_heavy;
+        vn.n_heavy = 0;
+      }
+    }
     cn.nchunks = (B + ccn - 1) / ccn;
     vn.nchunks = (B + cvn - 1) / cvn;
     cn.ldb = vn.ldb = ldbb;

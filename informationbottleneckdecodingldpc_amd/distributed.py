@@ -73,9 +73,10 @@ def _comm_device() -> torch.device:
 def broadcast_arrays(arrays: Dict[str, np.ndarray] | None, src: int = 0) -> Dict[str, np.ndarray]:
     """Broadcast a dict of numpy arrays from ``src`` to every rank (two collectives in total).
 
-    Non-source ranks pass ``None``. Key order, dtypes and shapes travel in a small header.
+    Non-source ranks pass ``None``. Key order, dtypes and shapes travel in a small header. An initialised
+    group of size 1 still runs the collectives (so a 1-GPU ``nccl`` group exercises the device path).
     """
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_initialized():
         return {k: np.ascontiguousarray(v) for k, v in (arrays or {}).items()}
     dev = _comm_device()
     rank = dist.get_rank()
@@ -119,13 +120,13 @@ def allreduce_counts(counts: Dict[str, int]) -> Dict[str, int]:
     """Sum integer counters over ranks (one all-reduce)."""
     keys = sorted(counts)
     t = torch.tensor([int(counts[k]) for k in keys], dtype=torch.int64, device=_comm_device())
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return dict(zip(keys, (int(x) for x in t.cpu().tolist())))
 
 
 def allreduce_max(x: float) -> float:
     t = torch.tensor([float(x)], dtype=torch.float64, device=_comm_device())
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

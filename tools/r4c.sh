@@ -5,7 +5,4 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_float.py -k "dataflow or fu
 echo "flowtests ok $(tail -1 $O/flowtests.log)" >> $O/summary.txt
 bash tools/ab_trees.sh r4c C3 head env:IBL_FUSED_FLOW=0 || exit 1
 bash tools/ab_trees.sh r4c C5 tree:abtrees/r02 head lib:ieee || exit 1
-bash tools/gpu_run.sh r4c tests || exit 1
-timeout -k 10 400 python -u -m pytest tests/test_gpu_float.py tests/test_gpu_ber_parity.py -k "converged_codewords_h5 or world_size_invariant" -s -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/prints.log 2>&1 || exit 1
-CONFIGS="C4 C2 C1" bash tools/gpu_run.sh r4c bench || exit 1
-CONFIGS="C3 C2" bash tools/gpu_run.sh r4c ftrace
+bash tools/gpu_run.sh r4c tests
