@@ -16,10 +16,11 @@ ARCH = os.environ.get("IBLDPC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wno-unused-result", "-Wno-pass-failed"]
-# per-source flags. float_kernels: the float messages are never NaN (finite channel LLRs, every operation
-# keeps them finite), so the kernels run with the IEEE mode bit off: v_min_f32 / v_max_f32 then take their
-# (|x|-modified) inputs directly instead of quieting each through a v_max x, x first
-SRC_FLAGS = {"float_kernels.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"]}
+# per-source flags (variants may override them). None by default: round 3 built float_kernels.hip with
+# -mno-amdgpu-ieee -fno-honor-nans, which made the device libraries' functions (blockDim, blockIdx, exp,
+# log) out-of-line calls in every float kernel (attribute mismatch: no inlining); the NaN-quieting those
+# flags removed is now skipped by inline min / max / med3 forms (float_kernels.hip vmin_aa ...)
+SRC_FLAGS = {}
 
 
 def _stale(out: str, deps) -> bool:
