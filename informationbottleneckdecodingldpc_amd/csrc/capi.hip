@@ -190,6 +190,7 @@ struct ibl_float {
   int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
   int32_t f_flow = 0, f_done_off = 0;            // task dataflow (FlFusedArgs::flow) and its LDS stamps
   uint64_t *f_cn_dep = nullptr, *f_vn_dep = nullptr;
+  int32_t* f_flow_err = nullptr;                  // FlFusedArgs::flow_err (kFlowErrWords, zeroed at create)
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -862,8 +863,10 @@ int fused_setup(ibl_float* h) {
       }
     int bpc2 = 0, block2 = 0;
     if (fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lds_flow, &bpc2, &block2) == hipSuccess && bpc2 == bpc) {
-      if ((rc = dupload(&h->f_cn_dep, cdep.data(), cdep.size())) || (rc = dupload(&h->f_vn_dep, vdep.data(), vdep.size())))
+      if ((rc = dupload(&h->f_cn_dep, cdep.data(), cdep.size())) || (rc = dupload(&h->f_vn_dep, vdep.data(), vdep.size())) ||
+          (rc = dalloc(&h->f_flow_err, kFlowErrWords)))
         return rc;
+      if (hipMemset(h->f_flow_err, 0, sizeof(int32_t) * kFlowErrWords) != hipSuccess) return fail(IBL_EHIP, "hipMemset failed");
       h->f_flow = 1;
       h->f_done_off = (int32_t)done_off;
       lds = lds_flow;
@@ -1098,6 +1101,16 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   return IBL_OK;
 }
 
+int ibl_float_flow_status(ibl_float* h, int32_t* words, int32_t n) {
+  if (!h || !words || n < 1) return fail(IBL_EINVAL, "NULL argument");
+  for (int32_t i = 0; i < n; ++i) words[i] = 0;
+  if (!h->f_flow_err) return IBL_OK;
+  HIPCHK(hipSetDevice(h->g->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(words, h->f_flow_err, sizeof(int32_t) * std::min<int32_t>(n, kFlowErrWords), hipMemcpyDeviceToHost));
+  return IBL_OK;
+}
+
 int ibl_float_fused_flow(const ibl_float* h, int32_t* flow) {
   if (!h || !flow) return fail(IBL_EINVAL, "NULL argument");
   int32_t fused = 0;
@@ -1111,7 +1124,7 @@ void ibl_float_destroy(ibl_float* h) {
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
   dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
-  dfree(h->f_cn_dep); dfree(h->f_vn_dep);
+  dfree(h->f_cn_dep); dfree(h->f_vn_dep); dfree(h->f_flow_err);
   delete h;
 }
 
@@ -1142,7 +1155,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
     // the phase trace describes the barrier schedule: tracing runs that one
     fa.flow = h->f_flow && !ftrace;
-    fa.done_off = h->f_done_off; fa.cn_dep = h->f_cn_dep; fa.vn_dep = h->f_vn_dep;
+    fa.done_off = h->f_done_off; fa.cn_dep = h->f_cn_dep; fa.vn_dep = h->f_vn_dep; fa.flow_err = h->f_flow_err;
     const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));

@@ -207,7 +207,13 @@ struct FlFusedArgs {
   int32_t flow, done_off;
   const uint64_t* cn_dep;
   const uint64_t* vn_dep;
+  // bounded waits: a wait that spins kFlowSpin times records {1, ticket, need, mask lo/hi, block, ballot
+  // lo/hi, the 128 stamps} here (first wave only) and every wave leaves the kernel: a broken dependency
+  // can never hang the GPU (ibl_float_flow_status reads it)
+  int32_t* flow_err;
 };
+constexpr int kFlowSpin = 1 << 20;
+constexpr int kFlowErrWords = 8 + 128;
 
 struct FlDecArgs {
   const void* vin0;         // ping-pong varnode inboxes, selected by parity of L

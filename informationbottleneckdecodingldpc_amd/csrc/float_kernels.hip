@@ -854,13 +854,25 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     int* done_v = done_c + 64;
     const int nc = a.n_cn_tasks, nv = a.n_vn_tasks;
     const int per = 2 * L + 1, tpg = nv + L * (nc + nv);
-    auto wait_for = [&](const int* done, uint64_t mask, int need) __attribute__((always_inline)) {
-      if (mask == 0) return;
-      for (;;) {
+    // true when every task in mask has a stamp >= need; false (diagnostics recorded) after kFlowSpin polls
+    auto wait_for = [&](const int* done, uint64_t mask, int need, int tk) __attribute__((always_inline)) {
+      if (mask == 0) return true;
+      for (int spin = 0; spin < kFlowSpin; ++spin) {
         const int st = __hip_atomic_load(done + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((__ballot(st >= need) & mask) == mask) break;
+        const uint64_t b = __ballot(st >= need);
+        if ((b & mask) == mask) return true;
+        if (spin == kFlowSpin - 1 && a.flow_err) {
+          if (lane == 0 && atomicCAS(a.flow_err, 0, 1) == 0) {
+            a.flow_err[1] = tk; a.flow_err[2] = need; a.flow_err[3] = (int)(uint32_t)mask;
+            a.flow_err[4] = (int)(uint32_t)(mask >> 32); a.flow_err[5] = (int)blockIdx.x;
+            a.flow_err[6] = (int)(uint32_t)b; a.flow_err[7] = (int)(uint32_t)(b >> 32);
+            const int* stamps = reinterpret_cast<const int*>(lds + a.done_off);
+            for (int i = 0; i < 128; ++i) a.flow_err[8 + i] = stamps[i];
+          }
+        }
         __builtin_amdgcn_s_sleep(1);
       }
+      return false;
     };
     auto publish = [&](int* done, int t, int P) __attribute__((always_inline)) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -874,7 +886,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       int r = tk - k * tpg;
       const int base = k * per;
       if (r < nv) {                        // send (local phase 0)
-        if (k > 0) wait_for(done_v, (uint64_t)1 << r, base - 1);
+        if (k > 0 && !wait_for(done_v, (uint64_t)1 << r, base - 1, tk)) break;
         send_task(r, grp);
         publish(done_v, r, base);
         continue;
@@ -883,7 +895,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       const int j = r / (nc + nv) + 1, q = r - (j - 1) * (nc + nv);
       if (q < nc) {                        // CN pass j (local phase 2j - 1)
         const int P = base + 2 * j - 1;
-        wait_for(done_v, a.cn_dep[q], P - 1);
+        if (!wait_for(done_v, a.cn_dep[q], P - 1, tk)) break;
         const bool do_par = a.unsat != nullptr;
         bool unsat = false;
         cn_task(q, valid, do_par, unsat);
@@ -891,7 +903,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
         publish(done_c, q, P);
       } else {                             // VN pass j (j < L) or the output (j == L), local phase 2j
         const int v = q - nc, P = base + 2 * j;
-        wait_for(done_c, a.vn_dep[v], P - 1);
+        if (!wait_for(done_c, a.vn_dep[v], P - 1, tk)) break;
         if (j < L) vn_task(v);
         else out_task(v, cw0, valid);
         publish(done_v, v, P);

@@ -436,6 +436,7 @@ def test_fused_dataflow_equals_phases_and_oracle(eng, monkeypatch, wlan_H, name,
         it = torch.zeros(1, dtype=torch.int32, device=DEV)
         out = dec.decode(torch.from_numpy(llr).to(DEV), early_stop=early, iters=it)
         torch.cuda.synchronize()
+        assert dec.flow_status()[0] == 0          # no dataflow wait reached its spin bound
         res[flow] = (out.double().cpu().numpy(), int(it.item()))
     np.testing.assert_array_equal(res["1"][0], res["0"][0])
     assert res["1"][1] == res["0"][1]
