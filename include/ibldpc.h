@@ -159,20 +159,6 @@ void ibl_float_destroy(ibl_float* h);
  */
 int ibl_float_set_path(ibl_float* h, int32_t path);
 int ibl_float_path_in_use(const ibl_float* h, int32_t* fused);
-/*
- * Schedule of the fused float kernel (no reference counterpart; results are identical): *flow = 1 when
- * its tasks run as a dataflow (each waits only for the tasks of the previous phase that touch its
- * message slots; codes with <= 64 check and variable tasks), 0 for barrier-separated phases (the
- * environment IBL_FUSED_FLOW=0 at create forces those) or when the fused kernel is not in use.
- */
-int ibl_float_fused_flow(const ibl_float* h, int32_t* flow);
-/*
- * Dataflow health (diagnostics; synchronises the device): words[0] = 1 if a task of the fused dataflow
- * ever waited past its spin bound (the kernel then leaves instead of hanging and that decode's outputs
- * are invalid), followed by {ticket, needed stamp, mask lo, mask hi, block, ballot lo, ballot hi, the
- * 128 done stamps}; all zero otherwise. n = words to copy (<= 136).
- */
-int ibl_float_flow_status(ibl_float* h, int32_t* words, int32_t n);
 int ibl_float_timing(ibl_float* h, int32_t enable);
 int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_launches, double* vn_ms, int32_t* vn_launches);
 

@@ -188,9 +188,6 @@ struct ibl_float {
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
-  int32_t f_flow = 0, f_done_off = 0;            // task dataflow (FlFusedArgs::flow) and its LDS stamps
-  uint64_t *f_cn_dep = nullptr, *f_vn_dep = nullptr;
-  int32_t* f_flow_err = nullptr;                  // FlFusedArgs::flow_err (kFlowErrWords, zeroed at create)
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -823,8 +820,6 @@ int fused_setup(ibl_float* h) {
   const char* s16e = getenv("IBL_FUSED_SLOT16");
   const bool slot16 = E < 65536 && lds16 <= (size_t)kLdsBytes && !(s16e && s16e[0] == '0');
   if (slot16) lds = lds16;
-  // task dataflow (FlFusedArgs::flow): 2 x 64 done stamps after the counters / slot indices
-  const size_t done_off = (lds + 15) / 16 * 16, lds_flow = done_off + 512;
   int min_dc = 1 << 30;
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
   if (lds > (size_t)kLdsBytes || min_dc < 2 || E == 0) return IBL_OK;
@@ -846,33 +841,6 @@ int fused_setup(ibl_float* h) {
   const std::vector<int32_t>& vn_task = ft.vn_task;
   h->f_ncn = (int32_t)(cn_task.size() / 4);
   h->f_nvn = (int32_t)(vn_task.size() / 4);
-  // Dependency masks of the task dataflow: the check tasks owning each variable task's slots and the
-  // transpose. Used when both sides have <= 64 tasks, the stamps fit and IBL_FUSED_FLOW is not 0 (A/B).
-  const char* fle = getenv("IBL_FUSED_FLOW");
-  if (h->f_ncn <= 64 && h->f_nvn <= 64 && lds_flow <= (size_t)kLdsBytes && !(fle && fle[0] == '0')) {
-    std::vector<uint64_t> cdep(h->f_ncn, 0), vdep(h->f_nvn, 0);
-    std::vector<int32_t> owner((size_t)E, -1);
-    for (int32_t c = 0; c < h->f_ncn; ++c)
-      for (int32_t e = cn_task[4 * c]; e < cn_task[4 * c] + cn_task[4 * c + 1] * cn_task[4 * c + 2]; ++e) owner[e] = c;
-    for (int32_t v = 0; v < h->f_nvn; ++v)
-      for (int32_t i = 0; i < vn_task[4 * v + 1] * vn_task[4 * v + 2]; ++i) {
-        const int32_t c = owner[ft.vn_slot[(size_t)vn_task[4 * v + 3] + i]];
-        if (c < 0) return fail(IBL_EHIP, "fused task tables: variable slot without a check task");
-        vdep[v] |= 1ull << c;
-        cdep[c] |= 1ull << v;
-      }
-    int bpc2 = 0, block2 = 0;
-    if (fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lds_flow, &bpc2, &block2) == hipSuccess && bpc2 == bpc) {
-      if ((rc = dupload(&h->f_cn_dep, cdep.data(), cdep.size())) || (rc = dupload(&h->f_vn_dep, vdep.data(), vdep.size())) ||
-          (rc = dalloc(&h->f_flow_err, kFlowErrWords)))
-        return rc;
-      if (hipMemset(h->f_flow_err, 0, sizeof(int32_t) * kFlowErrWords) != hipSuccess) return fail(IBL_EHIP, "hipMemset failed");
-      h->f_flow = 1;
-      h->f_done_off = (int32_t)done_off;
-      lds = lds_flow;
-    }
-    (void)hipGetLastError();
-  }
   h->f_lds = lds;
   h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
@@ -1101,30 +1069,11 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   return IBL_OK;
 }
 
-int ibl_float_flow_status(ibl_float* h, int32_t* words, int32_t n) {
-  if (!h || !words || n < 1) return fail(IBL_EINVAL, "NULL argument");
-  for (int32_t i = 0; i < n; ++i) words[i] = 0;
-  if (!h->f_flow_err) return IBL_OK;
-  HIPCHK(hipSetDevice(h->g->device));
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(words, h->f_flow_err, sizeof(int32_t) * std::min<int32_t>(n, kFlowErrWords), hipMemcpyDeviceToHost));
-  return IBL_OK;
-}
-
-int ibl_float_fused_flow(const ibl_float* h, int32_t* flow) {
-  if (!h || !flow) return fail(IBL_EINVAL, "NULL argument");
-  int32_t fused = 0;
-  ibl_float_path_in_use(h, &fused);
-  *flow = fused && h->f_flow ? 1 : 0;
-  return IBL_OK;
-}
-
 void ibl_float_destroy(ibl_float* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
   dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
-  dfree(h->f_cn_dep); dfree(h->f_vn_dep); dfree(h->f_flow_err);
   delete h;
 }
 
@@ -1153,9 +1102,6 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.ngroups = (B + cwl - 1) / cwl;
     fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
-    // the phase trace describes the barrier schedule: tracing runs that one
-    fa.flow = h->f_flow && !ftrace;
-    fa.done_off = h->f_done_off; fa.cn_dep = h->f_cn_dep; fa.vn_dep = h->f_vn_dep; fa.flow_err = h->f_flow_err;
     const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));

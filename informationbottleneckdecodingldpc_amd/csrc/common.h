@@ -201,19 +201,7 @@ struct FlFusedArgs {
   int32_t slot16;           // 1: vn_slot staged into LDS as 16-bit indices (after 4 counter words)
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED, -DIBL_FUSED_TRACE=1 builds): block 0's clock at
                             // every phase end of its first group, else nullptr
-  // task dataflow instead of phase barriers (flow = 1; both sides <= 64 tasks): cn_dep[c] = mask of the
-  // variable tasks touching check task c's slots, vn_dep[v] = mask of the check tasks touching variable
-  // task v's slots; done stamps (2 x 64 ints) follow the LDS counters / slot indices at byte done_off
-  int32_t flow, done_off;
-  const uint64_t* cn_dep;
-  const uint64_t* vn_dep;
-  // bounded waits: a wait that spins kFlowSpin times records {1, ticket, need, mask lo/hi, block, ballot
-  // lo/hi, the 128 stamps} here (first wave only) and every wave leaves the kernel: a broken dependency
-  // can never hang the GPU (ibl_float_flow_status reads it)
-  int32_t* flow_err;
 };
-constexpr int kFlowSpin = 1 << 20;
-constexpr int kFlowErrWords = 8 + 128;
 
 struct FlDecArgs {
   const void* vin0;         // ping-pong varnode inboxes, selected by parity of L

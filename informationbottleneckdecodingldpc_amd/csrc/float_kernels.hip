@@ -742,7 +742,6 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
   if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
-  if (a.flow && threadIdx.x < 128) reinterpret_cast<int*>(lds + a.done_off)[threadIdx.x] = -1;
   SlotIdx vs{nullptr, a.vn_slot};
   if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
     uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
@@ -841,76 +840,6 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       }
     }
   };
-
-  if (a.flow && L >= 1) {
-    // ---- task dataflow: no phase barriers. One ticket sequence per block walks its groups' phases in
-    // order (send; CN 1; VN 1; ...; CN L; output) and a task waits only for the tasks of the previous
-    // phase that touch its slots: check task c of phase P for the variable tasks in cn_dep[c] to have
-    // finished phase P-1, a variable / output task for the check tasks in vn_dep[v]; a group's send task v
-    // also for output task v of the previous group (same slots and channel slot). Waits only point back
-    // to smaller tickets, so the oldest unfinished ticket can always run. Done stamps: global phase
-    // index (group iteration k * (2L + 1) + local phase), written by lane 0 after the task's LDS stores.
-    int* done_c = reinterpret_cast<int*>(lds + a.done_off);
-    int* done_v = done_c + 64;
-    const int nc = a.n_cn_tasks, nv = a.n_vn_tasks;
-    const int per = 2 * L + 1, tpg = nv + L * (nc + nv);
-    // true when every task in mask has a stamp >= need; false (diagnostics recorded) after kFlowSpin polls
-    auto wait_for = [&](const int* done, uint64_t mask, int need, int tk) __attribute__((always_inline)) {
-      if (mask == 0) return true;
-      for (int spin = 0; spin < kFlowSpin; ++spin) {
-        const int st = __hip_atomic_load(done + lane, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint64_t b = __ballot(st >= need);
-        if ((b & mask) == mask) return true;
-        if (spin == kFlowSpin - 1 && a.flow_err) {
-          if (lane == 0 && atomicCAS(a.flow_err, 0, 1) == 0) {
-            a.flow_err[1] = tk; a.flow_err[2] = need; a.flow_err[3] = (int)(uint32_t)mask;
-            a.flow_err[4] = (int)(uint32_t)(mask >> 32); a.flow_err[5] = (int)blockIdx.x;
-            a.flow_err[6] = (int)(uint32_t)b; a.flow_err[7] = (int)(uint32_t)(b >> 32);
-            const int* stamps = reinterpret_cast<const int*>(lds + a.done_off);
-            for (int i = 0; i < 128; ++i) a.flow_err[8 + i] = stamps[i];
-          }
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      return false;
-    };
-    auto publish = [&](int* done, int t, int P) __attribute__((always_inline)) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(done + t, P, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    for (;;) {
-      const int tk = take_ticket(ctr, lane);
-      const int k = tk / tpg, grp = (int)blockIdx.x + k * (int)gridDim.x;
-      if (grp >= a.ngroups) break;
-      const int cw0 = grp * N, valid = a.B - cw0;
-      int r = tk - k * tpg;
-      const int base = k * per;
-      if (r < nv) {                        // send (local phase 0)
-        if (k > 0 && !wait_for(done_v, (uint64_t)1 << r, base - 1, tk)) break;
-        send_task(r, grp);
-        publish(done_v, r, base);
-        continue;
-      }
-      r -= nv;
-      const int j = r / (nc + nv) + 1, q = r - (j - 1) * (nc + nv);
-      if (q < nc) {                        // CN pass j (local phase 2j - 1)
-        const int P = base + 2 * j - 1;
-        if (!wait_for(done_v, a.cn_dep[q], P - 1, tk)) break;
-        const bool do_par = a.unsat != nullptr;
-        bool unsat = false;
-        cn_task(q, valid, do_par, unsat);
-        if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
-        publish(done_c, q, P);
-      } else {                             // VN pass j (j < L) or the output (j == L), local phase 2j
-        const int v = q - nc, P = base + 2 * j;
-        if (!wait_for(done_c, a.vn_dep[v], P - 1, tk)) break;
-        if (j < L) vn_task(v);
-        else out_task(v, cw0, valid);
-        publish(done_v, v, P);
-      }
-    }
-    return;
-  }
 
   // ---- phases separated by barriers
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {

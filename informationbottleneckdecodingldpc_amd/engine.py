@@ -185,19 +185,6 @@ class FloatDecoder:
         _lib.check(_lib.load().ibl_float_path_in_use(self._h, ctypes.byref(f)), "ibl_float_path_in_use")
         return bool(f.value)
 
-    def flow_status(self) -> list:
-        """``ibl_float_flow_status``: [0] = 1 if a dataflow wait ever hit its spin bound, then diagnostics."""
-        w = (ctypes.c_int32 * 136)()
-        _lib.check(_lib.load().ibl_float_flow_status(self._h, w, 136), "ibl_float_flow_status")
-        return list(w)
-
-    @property
-    def flow(self) -> bool:
-        """The fused kernel runs its tasks as a dataflow, not barrier-separated phases (``ibl_float_fused_flow``)."""
-        f = ctypes.c_int32()
-        _lib.check(_lib.load().ibl_float_fused_flow(self._h, ctypes.byref(f)), "ibl_float_fused_flow")
-        return bool(f.value)
-
     def decode(self, llr: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=None,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
         n = self.graph.edges.n_v
