@@ -140,10 +140,12 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
  * Replaces decode_OpenCL_min_sum (min_sum_decoder_irreg.py:221-287) and
  * decode_OpenCL_belief_propagation (bp_decoder_irreg.py:221-286).
  *   d_llr [N][B] channel LLRs (IBL_F32 / IBL_F64), d_out [N][B] APP LLRs (IBL_F32 / IBL_F64)
- * Precondition: no channel LLR is NaN.  +-inf is allowed (a known bit: every message a variable sends
- * is clamped to +-llr_max, its APP LLR is +-inf), and every message stays finite, so no operation
- * creates a NaN (BP box-plus inputs are clamped, |a+b| <= 2 llr_max).  The float kernels are built
- * for NaN-free data (-fno-honor-nans, IEEE mode off): a NaN input gives unspecified outputs.
+ * Precondition: no channel LLR is NaN.  Min-sum allows +-inf (a known bit: every message a variable
+ * sends is clamped to +-llr_max, its APP LLR is +-inf), and every message stays finite.  BP needs finite
+ * channel LLRs with |x| <= 354 (the first check pass box-pluses raw channel values; beyond that the
+ * reference's fp64 box-plus log((1 + e^(a+b)) / (e^a + e^b)) overflows to NaN, kernels_min_and_BP.cl:5-9);
+ * later box-plus inputs are clamped to +-llr_max.  The float kernels take min / max / median as single
+ * instructions that assume non-NaN operands: a NaN input gives unspecified outputs.
  */
 int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out,
                      int32_t out_dtype, int32_t early_stop, int32_t* d_iters, void* stream);

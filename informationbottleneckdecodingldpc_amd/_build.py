@@ -16,11 +16,12 @@ ARCH = os.environ.get("IBLDPC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wno-unused-result", "-Wno-pass-failed"]
-# per-source flags (variants may override them). None by default: round 3 built float_kernels.hip with
-# -mno-amdgpu-ieee -fno-honor-nans, which made the device libraries' functions (blockDim, blockIdx, exp,
-# log) out-of-line calls in every float kernel (attribute mismatch: no inlining); the NaN-quieting those
-# flags removed is now skipped by inline min / max / med3 forms (float_kernels.hip vmin_aa ...)
-SRC_FLAGS = {}
+# per-source flags (variants may override them). float_kernels: messages are never NaN (ibldpc.h's
+# precondition), so min / max / median need no NaN quieting (-fno-honor-nans: no v_max x, x in front of
+# operands loaded from memory). Round 3 also turned the IEEE mode off (-mno-amdgpu-ieee); that attribute
+# differs from the device libraries', which then stop inlining: blockDim / blockIdx / exp / log became
+# out-of-line calls in every float kernel. -fno-honor-nans alone keeps them inline.
+SRC_FLAGS = {"float_kernels.hip": ["-fno-honor-nans"]}
 
 
 def _stale(out: str, deps) -> bool:

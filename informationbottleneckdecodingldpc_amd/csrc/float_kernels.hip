@@ -43,47 +43,13 @@ template <> struct Vec<double> {
   __device__ static void set(T& v, int s, double x) { if (s == 0) v.x = x; else v.y = x; }
 };
 
-// fp32 min / max / median as single instructions. Messages are never NaN (ibldpc.h's precondition:
-// channel LLRs are finite or +-inf, and every operation keeps messages finite), so the compiler's
-// IEEE-mode quieting — a v_max_f32 x, x in front of every operand it cannot prove canonical, e.g. an LDS
-// or global load — is dead weight; these inline forms skip it (and take |x| as an input modifier)
-// without building the translation unit with the IEEE mode off: that attribute differs from the
-// device libraries', which then stop inlining (blockDim / blockIdx / exp / log became calls).
-__device__ __forceinline__ float vmin_aa(float a, float b) {   // min(|a|, |b|)
-  float r;
-  asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ float vmax_aa(float a, float b) {   // max(|a|, |b|)
-  float r;
-  asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ float vmin_a(float a, float b) {    // min(a, |b|)
-  float r;
-  asm("v_min_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ float vmed3_a(float a, float b, float c) {   // median(a, b, |c|)
-  float r;
-  asm("v_med3_f32 %0, %1, %2, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-__device__ __forceinline__ float vmed3_0(float a, float lm) {   // median(a, 0, lm) = clamp to [0, lm]
-  float r;
-  asm("v_med3_f32 %0, %1, 0, %2" : "=v"(r) : "v"(a), "s"(lm));
-  return r;
-}
-
 // sign(t) * min(llr_max, sign(t) * t)  (kernels_min_and_BP.cl:69,120) is the clamp of t to
 // [-llr_max, llr_max] for every non-NaN t, signed zeros included (sign(+-0) = +-0 gives +-0 back):
 // one v_med3_f32 in fp32 instead of the 3 compares, 3 selects, 2 products and a min of the literal
-// form; llr_max is wave-uniform (one SGPR read twice, once negated).
-__device__ __forceinline__ float clampllr(float t, float lm) {
-  float r;
-  asm("v_med3_f32 %0, %1, -%2, %2" : "=v"(r) : "v"(t), "s"(lm));
-  return r;
-}
+// form. Messages are never NaN (ibldpc.h's precondition), and this source is built with
+// -fno-honor-nans (_build.py): min / max / median then take their operands directly instead of
+// quieting each through a v_max x, x first.
+__device__ __forceinline__ float clampllr(float t, float lm) { return __builtin_amdgcn_fmed3f(t, -lm, lm); }
 __device__ __forceinline__ double clampllr(double t, double lm) { return fmin(fmax(t, -lm), lm); }
 
 // sign-bit arithmetic of the min-sum check node
@@ -94,10 +60,10 @@ template <> struct Bits<float> {
   __device__ static U of(float x) { return __float_as_uint(x); }
   __device__ static float from(U u) { return __uint_as_float(u); }
   // on raw messages: min(|a|, |b|), max(|a|, |b|), median(lo, hi, |x|), min(lo, |x|)
-  __device__ static float lo_aa(float a, float b) { return vmin_aa(a, b); }
-  __device__ static float hi_aa(float a, float b) { return vmax_aa(a, b); }
-  __device__ static float med3_a(float lo, float hi, float x) { return vmed3_a(lo, hi, x); }
-  __device__ static float lo_a(float lo, float x) { return vmin_a(lo, x); }
+  __device__ static float lo_aa(float a, float b) { return fminf(fabsf(a), fabsf(b)); }
+  __device__ static float hi_aa(float a, float b) { return fmaxf(fabsf(a), fabsf(b)); }
+  __device__ static float med3_a(float lo, float hi, float x) { return __builtin_amdgcn_fmed3f(lo, hi, fabsf(x)); }
+  __device__ static float lo_a(float lo, float x) { return fminf(lo, fabsf(x)); }
   // the compiler keeps v_and_b32 + v_or_b32 for this (gfx9 VOP3 takes no literal): one v_and_or_b32 with
   // the mask in an SGPR places a sign bit
   __device__ static U and_or(U a, U k, U b) {
@@ -132,11 +98,11 @@ __device__ __forceinline__ double boxplus(double a, double b, double lm) {
 __device__ __forceinline__ float boxplus(float a, float b, float lm) {
   constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
   const float aa = fabsf(a), ab = fabsf(b);
-  const float mn = vmin_aa(a, b);
+  const float mn = fminf(aa, ab);
   const float u = __builtin_amdgcn_exp2f(-(aa + ab) * kLog2e);
   const float v = __builtin_amdgcn_exp2f(-fabsf(aa - ab) * kLog2e);
   float mag = fmaf(kLn2, __builtin_amdgcn_logf(1.f + u) - __builtin_amdgcn_logf(1.f + v), mn);
-  mag = vmed3_0(mag, lm);   // rounding may leave -ulp for tiny min; clamp to [0, lm] (:69)
+  mag = __builtin_amdgcn_fmed3f(mag, 0.f, lm);  // rounding may leave -ulp for tiny min; clamp to [0, lm] (:69)
   return ((a < 0.f) != (b < 0.f)) ? -mag : mag;
 }
 
