@@ -27,6 +27,14 @@
 
 namespace ibl {
 
+// Work-item geometry from the hardware registers and the dispatch packet. This source is built with the
+// IEEE mode off (_build.py), an attribute the device libraries do not share, so HIP's threadIdx /
+// blockIdx / blockDim / gridDim — calls into them — would stay out-of-line calls in every kernel.
+__device__ __forceinline__ int fl_tid() { return (int)__builtin_amdgcn_workitem_id_x(); }
+__device__ __forceinline__ int fl_bid() { return (int)__builtin_amdgcn_workgroup_id_x(); }
+__device__ __forceinline__ int fl_bdim() { return (int)__builtin_amdgcn_workgroup_size_x(); }
+__device__ __forceinline__ int fl_gdim() { return (int)(__builtin_amdgcn_grid_size_x() / __builtin_amdgcn_workgroup_size_x()); }
+
 template <typename F> struct Vec;
 template <> struct Vec<float> {
   static constexpr int N = 4;
@@ -47,8 +55,8 @@ template <> struct Vec<double> {
 // [-llr_max, llr_max] for every non-NaN t, signed zeros included (sign(+-0) = +-0 gives +-0 back):
 // one v_med3_f32 in fp32 instead of the 3 compares, 3 selects, 2 products and a min of the literal
 // form. Messages are never NaN (ibldpc.h's precondition), and this source is built with
-// -fno-honor-nans (_build.py): min / max / median then take their operands directly instead of
-// quieting each through a v_max x, x first.
+// -fno-honor-nans and the IEEE mode off (_build.py): min / max / median then take their operands
+// directly instead of quieting each through a v_max x, x first.
 __device__ __forceinline__ float clampllr(float t, float lm) { return __builtin_amdgcn_fmed3f(t, -lm, lm); }
 __device__ __forceinline__ double clampllr(double t, double lm) { return fmin(fmax(t, -lm), lm); }
 
@@ -404,21 +412,21 @@ static int fl_fused_block(int kind, int prec, int cmax) {
 // block's waves by LDS tickets (take_ticket): ticket k -> item b*wpb + k % wpb + nw * (k / wpb).
 __device__ __forceinline__ int fl_next_item(int* ctr, int lane, int wpb, int nw) {
   const int k = take_ticket(ctr, lane);
-  return (int)blockIdx.x * wpb + (k % wpb) + nw * (k / wpb);
+  return (int)fl_bid() * wpb + (k % wpb) + nw * (k / wpb);
 }
 
 template <int KIND, typename F, int MAXD>
 __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_cn(FlArgs a) {
-  const int lane = threadIdx.x & 63;
+  const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
   constexpr int CWL = Vec<F>::N;
   constexpr int CH = 64 * CWL;
   const bool do_par = a.unsat != nullptr;
   bool unsat = false;
   __shared__ int ctr;
-  if (threadIdx.x == 0) ctr = 0;
+  if (fl_tid() == 0) ctr = 0;
   __syncthreads();
-  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_nodes * a.nchunks;
+  const int wpb = fl_bdim() >> 6, nw = fl_gdim() * wpb, nitems = a.n_nodes * a.nchunks;
   for (;;) {
     const int item = fl_next_item(&ctr, lane, wpb, nw);
     if (item >= nitems) break;
@@ -435,19 +443,19 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_cn(FlArg
     }
   }
   if (do_par && __ballot(unsat) != 0ull && lane == 0)
-    atomicOr(&a.unsat[(blockIdx.x * wpb + (threadIdx.x >> 6)) & (kShards - 1)], 1);
+    atomicOr(&a.unsat[(fl_bid() * wpb + (fl_tid() >> 6)) & (kShards - 1)], 1);
 }
 
 template <typename F, int MAXD>
 __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
-  const int lane = threadIdx.x & 63;
+  const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
   constexpr int CWL = Vec<F>::N;
   constexpr int CH = 64 * CWL;
   __shared__ int ctr;
-  if (threadIdx.x == 0) ctr = 0;
+  if (fl_tid() == 0) ctr = 0;
   __syncthreads();
-  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_nodes * a.nchunks;
+  const int wpb = fl_bdim() >> 6, nw = fl_gdim() * wpb, nitems = a.n_nodes * a.nchunks;
   for (;;) {
     const int item = fl_next_item(&ctr, lane, wpb, nw);
     if (item >= nitems) break;
@@ -475,8 +483,8 @@ __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
   const F* vin = reinterpret_cast<const F*>((L & 1) ? a.vin1 : a.vin0);
   const F* ch = reinterpret_cast<const F*>(a.ch);
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+  const int lane = fl_tid() & 63;
+  const int gw = fl_bid() * (fl_bdim() >> 6) + (fl_tid() >> 6), nw = fl_gdim() * (fl_bdim() >> 6);
   const int nitems = a.n_nodes * a.nchunks;
   for (int item = gw; item < nitems; item += nw) {
     const int n = __builtin_amdgcn_readfirstlane(item / a.nchunks);
@@ -524,7 +532,7 @@ __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
 template <typename F>
 __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb) {
   const size_t total = (size_t)n * ldb;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < total; i += (size_t)fl_gdim() * fl_bdim()) {
     const int row = (int)(i / ldb);
     const int b = (int)(i - (size_t)row * ldb);
     F v = F(0);
@@ -548,7 +556,7 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
   __shared__ F tile[P * RW];
   const int ngroups = (B + N - 1) / N;
   const int ptiles = (n + P - 1) / P, gtiles = (ngroups + G - 1) / G;
-  for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
+  for (int t = fl_bid(); t < ptiles * gtiles; t += fl_gdim()) {
     const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
     __syncthreads();
     // all of a thread's loads issued before its LDS stores (256 threads: P*G*N/256 elements each)
@@ -556,7 +564,7 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
     F val[kPer];
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
-      const int i = threadIdx.x + it * 256;
+      const int i = fl_tid() + it * 256;
       const int r = i / (G * N), c = i - r * (G * N);
       const int b = g0 * N + c;
       val[it] = F(0);
@@ -568,12 +576,12 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
     }
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
-      const int i = threadIdx.x + it * 256;
+      const int i = fl_tid() + it * 256;
       const int r = i / (G * N), c = i - r * (G * N);
       tile[r * RW + c] = val[it];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < P * G; i += blockDim.x) {
+    for (int i = fl_tid(); i < P * G; i += fl_bdim()) {
       const int g = i / P, p = i - g * P;
       if (p0 + p < n && g0 + g < ngroups) {
         typename V::T o;
@@ -592,7 +600,7 @@ __global__ void fl_send(FlArgs a) {
   F* dst = reinterpret_cast<F*>(a.out);
   const int per = a.ldb / 4;
   const size_t total = (size_t)a.n_nodes * per;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < total; i += (size_t)fl_gdim() * fl_bdim()) {
     const int n = (int)(i / per);
     const int b4 = (int)(i - (size_t)n * per) * 4;
     if (b4 >= a.B) continue;
@@ -700,31 +708,31 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   // tasks) measured 1.29x slower on C3 (WLAN N=1944) — the per-task latency, not the body, dominates
   constexpr int NCs = N, h = 0;
   int* ctr = reinterpret_cast<int*>(chL + a.n_v);
-  const int lane = threadIdx.x & 63;
+  const int lane = fl_tid() & 63;
   const F lm = (F)a.llr_max;
   int L = a.imax - 1;
   if (a.dL) {
     L = __builtin_amdgcn_readfirstlane(*a.dL);
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
-  if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+  if (fl_tid() < 2) ctr[fl_tid()] = 0;
   SlotIdx vs{nullptr, a.vn_slot};
   if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
     uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
-    for (int i = threadIdx.x; i < a.n_e; i += blockDim.x) s16[i] = (uint16_t)a.vn_slot[i];
+    for (int i = fl_tid(); i < a.n_e; i += fl_bdim()) s16[i] = (uint16_t)a.vn_slot[i];
     vs.s16 = s16;
   }
   __syncthreads();
   int ph = 0;
-  const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
+  const int shard = (int)((fl_bid() * (fl_bdim() >> 6) + (fl_tid() >> 6)) & (kShards - 1));
   // one phase: tasks dealt by ticket; the next phase's counter is reset while this one runs
 #ifndef IBL_FUSED_TRACE
 #define IBL_FUSED_TRACE 0
 #endif
   // phase trace of block 0's first group (diagnostic builds): kFlTraceWords per phase (common.h)
-  const int wv = threadIdx.x >> 6;
+  const int wv = fl_tid() >> 6;
   constexpr int TW = kFlTraceWords;
-  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && blockIdx.x == 0 && lane == 0) ? a.trace : nullptr;
+  uint64_t* tr = (IBL_FUSED_TRACE && a.trace && fl_bid() == 0 && lane == 0) ? a.trace : nullptr;
   if (IBL_FUSED_TRACE && tr && wv == 0) tr[0] = __builtin_readcyclecounter();
   // ---- task bodies (one task = up to 64 same-degree nodes, lane i = node i) ----
   // send: every variable's channel slot and its edge slots
@@ -810,7 +818,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   // ---- phases separated by barriers
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
-    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    if (fl_tid() == 0) ctr[(ph + 1) & 1] = 0;
     int taken = 0;
     for (;;) {
       const int t = take_ticket(c, lane);
@@ -836,7 +844,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       if (tr && wv == 0) tr[TW * ph] = __builtin_readcyclecounter();
     }
   };
-  for (int grp = blockIdx.x; grp < a.ngroups; grp += gridDim.x) {
+  for (int grp = fl_bid(); grp < a.ngroups; grp += fl_gdim()) {
     const int cw0 = grp * N;
     const int valid = a.B - cw0;
     phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { send_task(t, grp); });

@@ -48,11 +48,11 @@ VARIANTS = {
     "nc22": ["IBL_NC_CN=2", "IBL_NC_VN=2", 'IBL_SCHED_FILE="ib_sched_nc22.inc"'],
     "nc33": ["IBL_NC_CN=3", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc33.inc"'],
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
-    # float kernels built with the IEEE mode bit off and NaNs not honoured (the round-3 float build flags)
-    "noieee": [],
+    # float kernels built with NaNs not honoured but the IEEE mode bit on
+    "ieeeon": [],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
-SRC_FLAGS = {"noieee": {"float_kernels.hip": ["-mno-amdgpu-ieee", "-fno-honor-nans"]}}
+SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
 # gen_sched.py arguments of the variants that need their own schedule file
 SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3",
               "s2n": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0"}
