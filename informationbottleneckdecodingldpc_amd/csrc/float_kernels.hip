@@ -72,6 +72,7 @@ template <> struct Bits<float> {
   __device__ static float hi_aa(float a, float b) { return fmaxf(fabsf(a), fabsf(b)); }
   __device__ static float med3_a(float lo, float hi, float x) { return __builtin_amdgcn_fmed3f(lo, hi, fabsf(x)); }
   __device__ static float lo_a(float lo, float x) { return fminf(lo, fabsf(x)); }
+  __device__ static float lo(float a, float b) { return fminf(a, b); }
   // the compiler keeps v_and_b32 + v_or_b32 for this (gfx9 VOP3 takes no literal): one v_and_or_b32 with
   // the mask in an SGPR places a sign bit
   __device__ static U and_or(U a, U k, U b) {
@@ -91,6 +92,7 @@ template <> struct Bits<double> {
   __device__ static double hi_aa(double a, double b) { return fmax(fabs(a), fabs(b)); }
   __device__ static double med3_a(double lo, double hi, double x) { return fmax(lo, fmin(hi, fabs(x))); }
   __device__ static double lo_a(double lo, double x) { return fmin(lo, fabs(x)); }
+  __device__ static double lo(double a, double b) { return fmin(a, b); }
   __device__ static U and_or(U a, U k, U b) { return (a & k) | b; }
   __device__ static U sign_mask() { return kSign; }
 };
@@ -181,12 +183,60 @@ __device__ __forceinline__ bool syndrome_bit(const F (&m)[D][NC], int s) {
 }
 
 // Check-node body on the inputs m of NC codewords (min-sum or BP); put(w, o) receives output w (any
-// order of w).
+// order of w). IBL_MS_PS = 0 keeps the (min, second min) form for every degree (A/B).
+#ifndef IBL_MS_PS
+#define IBL_MS_PS 1
+#endif
 template <int KIND, typename F, int D, int NC, class Put>
 __device__ __forceinline__ void fl_cn_body(const F (&m)[D][NC], F lm, Put&& put) {
   constexpr int N = NC;
   F o[N];
-  if constexpr (KIND == 0) {
+  if constexpr (KIND == 0 && D <= 8 && IBL_MS_PS) {
+    // min-sum (kernels_min_and_BP.cl:156-162) with prefix / suffix minima: |out_w| = min over the others =
+    // min(P_w, S_{w+1}), P_w = min |m_0..m_{w-1}|, S_j = min |m_j..m_{D-1}| — 3(D-2) v_min (|x| as an input
+    // modifier) instead of the running (min, second min) pair plus a compare and a select per output
+    // (4D - 2); min only selects, so the outputs are the same bits. Signs: XOR of the others' sign bits
+    // (sign_xor ^ own), placed with one v_and_or_b32. A zero input gives every other output +-0 and its own
+    // the others' minimum, as the reference's sign(0) = 0 fold; the same tiny-LLR assumption as below.
+    using Bt = Bits<F>;
+    using U = typename Bt::U;
+    const U ks = Bt::sign_mask();
+    U sg[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) sg[s] = sign_xor<F, D>(m, s);
+    auto emit = [&](int w, const F (&mag)[N]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int s = 0; s < N; ++s) o[s] = Bt::from(Bt::and_or(sg[s] ^ Bt::of(m[w][s]), ks, Bt::of(mag[s])));
+      put(w, o);
+    };
+    if constexpr (D == 2) {
+      F a[N], b[N];
+#pragma unroll
+      for (int s = 0; s < N; ++s) { a[s] = fabs(m[1][s]); b[s] = fabs(m[0][s]); }
+      emit(0, a);
+      emit(1, b);
+    } else {
+      F S[D][N], P[N], mg[N];   // S[j] for j = 1..D-2
+#pragma unroll
+      for (int s = 0; s < N; ++s) S[D - 2][s] = Bt::lo_aa(m[D - 2][s], m[D - 1][s]);
+#pragma unroll
+      for (int j = D - 3; j >= 1; --j)
+#pragma unroll
+        for (int s = 0; s < N; ++s) S[j][s] = Bt::lo_a(S[j + 1][s], m[j][s]);
+      emit(0, S[1]);
+#pragma unroll
+      for (int s = 0; s < N; ++s) P[s] = fabs(m[0][s]);
+#pragma unroll
+      for (int w = 1; w <= D - 2; ++w) {
+#pragma unroll
+        for (int s = 0; s < N; ++s) mg[s] = w + 1 <= D - 2 ? Bt::lo(P[s], S[w + 1][s]) : Bt::lo_a(P[s], m[D - 1][s]);
+        emit(w, mg);
+#pragma unroll
+        for (int s = 0; s < N; ++s) P[s] = Bt::lo_a(P[s], m[w][s]);
+      }
+      emit(D - 1, P);
+    }
+  } else if constexpr (KIND == 0) {
     // min-sum (kernels_min_and_BP.cl:156-162): the fold t = sgn(m t) min(|t|, |m|) over the others of
     // output w only selects values, so |out_w| = min over the others = mn1, or mn2 where |m_w| is the
     // minimum (on a tie mn2 == mn1), and its sign is the XOR of the others' sign bits. A zero input
@@ -617,6 +667,9 @@ __global__ void fl_send(FlArgs a) {
 }
 
 // ------------------------------------------------------------ fused on-chip decoder
+#ifndef IBL_FUSED_STATIC1
+#define IBL_FUSED_STATIC1 1
+#endif
 // For codes whose messages fit in LDS ((E + N) * 16 B <= 160 KiB, e.g. WLAN N=1944: 142.6 KB), one
 // workgroup decodes Vec<F>::N codewords (4 fp32 / 2 fp64, one 16-byte slot per edge and per
 // variable) through ALL iterations without touching HBM: the flooding schedule of
@@ -715,7 +768,9 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     L = __builtin_amdgcn_readfirstlane(*a.dL);
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
-  if (fl_tid() < 2) ctr[fl_tid()] = 0;
+  // phase tickets start after the waves' static first tasks (see phase)
+  const int wpb = fl_bdim() >> 6;
+  if (fl_tid() < 2) ctr[fl_tid()] = IBL_FUSED_STATIC1 ? wpb : 0;
   SlotIdx vs{nullptr, a.vn_slot};
   if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
     uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
@@ -816,12 +871,15 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   };
 
   // ---- phases separated by barriers
+  // A wave's first task of a phase is its wave index (no ticket: the LDS atomic's round trip, with 16
+  // waves on one counter, was on every phase's critical path — C3 runs one check task per wave); further
+  // tasks come from the phase's ticket counter, which starts at the wave count.
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
-    if (fl_tid() == 0) ctr[(ph + 1) & 1] = 0;
+    if (fl_tid() == 0) ctr[(ph + 1) & 1] = IBL_FUSED_STATIC1 ? wpb : 0;
     int taken = 0;
     for (;;) {
-      const int t = take_ticket(c, lane);
+      const int t = (IBL_FUSED_STATIC1 && taken == 0) ? wv : take_ticket(c, lane);
       if (t >= ntasks) break;
       if constexpr (IBL_FUSED_TRACE) {
         if (tr && taken == 0) tr[TW * ph + 33 + wv] = __builtin_readcyclecounter();
