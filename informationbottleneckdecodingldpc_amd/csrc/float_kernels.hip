@@ -595,50 +595,61 @@ __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int 
 }
 
 // channel staging for the fused decoder: user LLRs [N][B] -> [group][variable position] 16-byte slots
-// (Vec<F>::N codewords of variable perm[pos]), zero padded past B
-// Tiled through LDS (64 positions x 32 groups): rows read along the codewords, slots written along the
-// positions, both coalesced; tile rows padded by one element.
+// (Vec<F>::N codewords of variable perm[pos]), zero padded past B. A slot is N consecutive codewords of
+// one row, so each cell is ONE 16-byte load (rows read along the codewords, 512 B per row and tile) and
+// the LDS tile only transposes whole cells: 64 positions x 32 groups, rows padded by one cell (the
+// position-major reads of a ds_read_b128 lane group then hit 16 distinct 4-bank groups); the slots are
+// written along the positions (1 KiB per wave). Non-vector inputs (other dtype, B % N != 0, unaligned)
+// load element by element.
 template <typename F>
 __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm,
                                                   typename Vec<F>::T* dst) {
   using V = Vec<F>;
-  constexpr int N = V::N, P = 64, G = 32, RW = G * N + 1;
-  __shared__ F tile[P * RW];
+  using VT = typename V::T;
+  constexpr int N = V::N, P = 64, G = 32, RW = G + 1;
+  __shared__ VT tile[P * RW];
   const int ngroups = (B + N - 1) / N;
   const int ptiles = (n + P - 1) / P, gtiles = (ngroups + G - 1) / G;
+  const int own = sizeof(F) == 4 ? kF32 : kF64;
+  const bool vec = in_dtype == own && (B % N) == 0 && (reinterpret_cast<uintptr_t>(x) % sizeof(VT)) == 0;
   for (int t = fl_bid(); t < ptiles * gtiles; t += fl_gdim()) {
     const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
     __syncthreads();
-    // all of a thread's loads issued before its LDS stores (256 threads: P*G*N/256 elements each)
-    constexpr int kPer = P * G * N / 256;
-    F val[kPer];
+    constexpr int kPer = P * G / 256;   // cells per thread, all loads issued before the LDS stores
+    VT v[kPer];
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
-      const int r = i / (G * N), c = i - r * (G * N);
-      const int b = g0 * N + c;
-      val[it] = F(0);
-      if (p0 + r < n && b < B) {
-        const size_t k = (size_t)perm[p0 + r] * B + b;
-        val[it] = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
-        val[it] = val[it] + F(0);   // -0 -> +0 (equal values; see sign_xor)
+      const int r = i / G, c = i - r * G;
+      const int p = p0 + r, g = g0 + c;
+#pragma unroll
+      for (int s = 0; s < N; ++s) V::set(v[it], s, F(0));
+      if (p < n && g < ngroups) {
+        const size_t k = (size_t)perm[p] * B + (size_t)g * N;
+        if (vec) {
+          v[it] = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(x) + k);
+        } else {
+#pragma unroll
+          for (int s = 0; s < N; ++s)
+            if (g * N + s < B)
+              V::set(v[it], s, in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k + s]
+                                                : (F)reinterpret_cast<const double*>(x)[k + s]);
+        }
       }
     }
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
-      const int r = i / (G * N), c = i - r * (G * N);
-      tile[r * RW + c] = val[it];
+      const int r = i / G, c = i - r * G;
+      VT o;
+#pragma unroll
+      for (int s = 0; s < N; ++s) V::set(o, s, V::get(v[it], s) + F(0));   // -0 -> +0 (see sign_xor)
+      tile[r * RW + c] = o;
     }
     __syncthreads();
     for (int i = fl_tid(); i < P * G; i += fl_bdim()) {
       const int g = i / P, p = i - g * P;
-      if (p0 + p < n && g0 + g < ngroups) {
-        typename V::T o;
-#pragma unroll
-        for (int s = 0; s < N; ++s) V::set(o, s, tile[p * RW + g * N + s]);
-        dst[(size_t)(g0 + g) * n + p0 + p] = o;
-      }
+      if (p0 + p < n && g0 + g < ngroups) dst[(size_t)(g0 + g) * n + p0 + p] = tile[p * RW + g];
     }
   }
 }

@@ -1066,45 +1066,54 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
 }
 
 // channel staging for the fused decoder: user [N][B] (u8 / i32) -> chT [group][position] dwords of 8
-// nibbles, positions in variable-task order (perm[pos] = node), so a task's lanes read consecutive dwords
-// Tiled through LDS (64 positions x 512 codewords): rows are read along the codewords (coalesced), the
-// dwords are written along the positions (coalesced); tile rows padded by one dword (conflict-free reads).
+// nibbles, positions in variable-task order (perm[pos] = node), so a task's lanes read consecutive dwords.
+// A cell (position, group) is 8 consecutive codewords of one row: one 8-byte load for aligned u8 rows
+// (two 16-byte loads for aligned i32), packed to nibbles in registers (values clamped to 15: cluster ids
+// of the fast path's 16-level alphabet); the LDS tile (64 positions x 64 groups, rows padded by one dword)
+// only transposes cells, and the dwords are written along the positions.
 __global__ __launch_bounds__(256) void ib_stage_t(const void* ch, int dtype, int n, int B, const int32_t* perm,
                                                   uint32_t* chT) {
-  constexpr int P = 64, G = 64, RW = 2 * G + 1;   // RW: dwords per tile row (4 codewords each) + pad
+  constexpr int P = 64, G = 64, RW = G + 1;
   __shared__ uint32_t tile[P * RW];
   const int ngroups = (B + 7) >> 3;
   const int ptiles = (n + P - 1) / P, gtiles = (ngroups + G - 1) / G;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(ch);
+  const bool vec = (B & 7) == 0 && (dtype == kU8 ? (base & 7) == 0 : (base & 15) == 0);
+  auto nib = [](uint32_t x) {   // 4 bytes (each clamped to 15) -> 4 nibbles
+    uint32_t y = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) y |= min((x >> (8 * s)) & 0xFFu, 15u) << (4 * s);
+    return y;
+  };
   for (int t = blockIdx.x; t < ptiles * gtiles; t += gridDim.x) {
     const int p0 = (t % ptiles) * P, g0 = (t / ptiles) * G;
     __syncthreads();
-    // all of a thread's loads issued before its LDS stores (256 threads: 32 dwords of 4 codewords each);
-    // u8 rows whose 4-codeword words are aligned (B % 4 == 0) load one dword per word
-    constexpr int kPer = P * 2 * G / 256;
+    constexpr int kPer = P * G / 256;   // cells per thread, all loads issued before the LDS stores
     uint32_t w[kPer];
-    const bool words = dtype == kU8 && (B & 3) == 0 && (reinterpret_cast<uintptr_t>(ch) & 3) == 0;
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = threadIdx.x + it * 256;
-      const int r = i / (2 * G), c = i - r * (2 * G);
+      const int r = i / G, c = i - r * G;
+      const int p = p0 + r, g = g0 + c;
       w[it] = 0;
-      if (p0 + r < n) {
-        const size_t row = (size_t)perm[p0 + r] * B;
-        const int cw = g0 * 8 + 4 * c;
-        if (words) {
-          if (cw < B) w[it] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(ch) + row + cw);
+      if (p < n && g < ngroups) {
+        const size_t k = (size_t)perm[p] * B + (size_t)g * 8;
+        if (vec && dtype == kU8) {
+          const uint2 b = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(ch) + k);
+          w[it] = nib(b.x) | (nib(b.y) << 16);
+        } else if (vec) {
+          const int4* q = reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(ch) + k);
+          const int4 a = q[0], b = q[1];
+          const int e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+          for (int s = 0; s < 8; ++s) w[it] |= (uint32_t)min(max(e[s], 0), 15) << (4 * s);
         } else {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            if (cw + s < B) {
-              uint32_t x;
-              if (dtype == kU8) {
-                x = reinterpret_cast<const uint8_t*>(ch)[row + cw + s];
-              } else {
-                const int32_t y = reinterpret_cast<const int32_t*>(ch)[row + cw + s];
-                x = (uint32_t)min(max(y, 0), 255);
-              }
-              w[it] |= x << (8 * s);
+          for (int s = 0; s < 8; ++s) {
+            if (g * 8 + s < B) {
+              const int y = dtype == kU8 ? (int)reinterpret_cast<const uint8_t*>(ch)[k + s]
+                                         : reinterpret_cast<const int32_t*>(ch)[k + s];
+              w[it] |= (uint32_t)min(max(y, 0), 15) << (4 * s);
             }
           }
         }
@@ -1113,22 +1122,13 @@ __global__ __launch_bounds__(256) void ib_stage_t(const void* ch, int dtype, int
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = threadIdx.x + it * 256;
-      const int r = i / (2 * G), c = i - r * (2 * G);
-      // bytes clamped to 15 (cluster ids of the fast path's 16-level alphabet)
-      const uint32_t x = w[it];
-      uint32_t y = 0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) y |= min((x >> (8 * s)) & 0xFFu, 15u) << (8 * s);
-      tile[r * RW + c] = y;
+      const int r = i / G, c = i - r * G;
+      tile[r * RW + c] = w[it];
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P * G; i += blockDim.x) {
       const int g = i / P, p = i - g * P;
-      if (p0 + p < n && g0 + g < ngroups) {
-        const uint32_t lo = tile[p * RW + 2 * g], hi = tile[p * RW + 2 * g + 1];
-        auto nib4 = [](uint32_t x) { return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u); };
-        chT[(size_t)(g0 + g) * n + p0 + p] = nib4(lo) | (nib4(hi) << 16);
-      }
+      if (p0 + p < n && g0 + g < ngroups) chT[(size_t)(g0 + g) * n + p0 + p] = tile[p * RW + g];
     }
   }
 }
