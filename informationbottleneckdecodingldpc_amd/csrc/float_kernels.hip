@@ -823,9 +823,26 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       }
     }
   };
+  // variable update: heavy-degree tasks come as two half-slot tasks (vn_utask), so the phase's longest
+  // bodies (WLAN's degree-11 variables: 64 order-preserving sums of 4 codewords per lane) are spread over
+  // twice the waves instead of setting the phase's length
   auto vn_task = [&](int t) __attribute__((always_inline)) {
-    const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
-    const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
+    const int pos = sload(a.vn_utask, 4 * t), rec = sload(a.vn_utask, 4 * t + 1);
+    const int d = sload(a.vn_utask, 4 * t + 2), sf = sload(a.vn_utask, 4 * t + 3);
+    const int cnt = rec & 0xFFFF, half = rec >> 16;
+    if constexpr (N == 4) {
+      if (half) {
+        if (lane < cnt) {
+          switch (d) {
+#define X(D) case D: if constexpr (D >= kFlSplitD && D <= VMAX) fused_vn_item<F, D, 2>(msg, chL, vs, pos + lane, sf, cnt, lane, half - 1, lm); break;
+            FL_DEG_CASES(X)
+#undef X
+            default: break;
+          }
+        }
+        return;
+      }
+    }
     if (lane < cnt) {
       switch (d) {
         case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
@@ -923,7 +940,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       phase(a.n_cn_tasks, [&](int t) __attribute__((always_inline)) { cn_task(t, valid, do_par, unsat); });
       if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
       if (j == L) break;
-      phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { vn_task(t); });
+      phase(a.n_vn_utasks, [&](int t) __attribute__((always_inline)) { vn_task(t); });
     }
     phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { out_task(t, cw0, valid); });
     tr = nullptr;   // trace the first group only
