@@ -188,8 +188,6 @@ struct ibl_float {
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
-  int32_t* f_vn_utask = nullptr;                 // FlFusedArgs::vn_utask
-  int32_t f_nvu = 0;
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -843,23 +841,6 @@ int fused_setup(ibl_float* h) {
   const std::vector<int32_t>& vn_task = ft.vn_task;
   h->f_ncn = (int32_t)(cn_task.size() / 4);
   h->f_nvn = (int32_t)(vn_task.size() / 4);
-  // variable-update tasks: fp32 tasks of degree >= kFlSplitD as two half-slot tasks (IBL_FUSED_VSPLIT=0: none)
-  {
-    const char* vse = getenv("IBL_FUSED_VSPLIT");
-    const bool split = h->prec == kF32 && !(vse && vse[0] == '0');
-    std::vector<int32_t> ut;
-    for (int32_t t = 0; t < h->f_nvn; ++t) {
-      const int32_t* r = &vn_task[4 * t];
-      if (split && r[2] >= kFlSplitD) {
-        ut.insert(ut.end(), {r[0], r[1] | (1 << 16), r[2], r[3]});
-        ut.insert(ut.end(), {r[0], r[1] | (2 << 16), r[2], r[3]});
-      } else {
-        ut.insert(ut.end(), {r[0], r[1], r[2], r[3]});
-      }
-    }
-    if ((rc = dupload(&h->f_vn_utask, ut.data(), ut.size()))) return rc;
-    h->f_nvu = (int32_t)(ut.size() / 4);
-  }
   h->f_lds = lds;
   h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
@@ -1092,7 +1073,7 @@ void ibl_float_destroy(ibl_float* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
-  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot); dfree(h->f_vn_utask);
+  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
   delete h;
 }
 
@@ -1117,7 +1098,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.ch = h->chf; fa.cn_task = h->f_cn_task; fa.vn_task = h->f_vn_task; fa.vn_node = h->f_vn_node;
     fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
     fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
-    fa.n_vn_tasks = h->f_nvn; fa.vn_utask = h->f_vn_utask; fa.n_vn_utasks = h->f_nvu; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
+    fa.n_vn_tasks = h->f_nvn; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
     fa.ngroups = (B + cwl - 1) / cwl;
     fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group

@@ -51,7 +51,6 @@ __host__ __device__ constexpr int cn_ncols(int D) { return (D >= 5 && D <= 8) ? 
 __host__ __device__ constexpr int vn_ncols(int D) { return (D >= 6 && D <= 8) ? IBL_NC_VN : 0; }
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
 constexpr int kMaxD = 16;
-constexpr int kFlSplitD = 8;     // fused float kernel: variable degrees from here on update in half-slot tasks
 constexpr int kLightD = 4;        // nodes up to this degree run with a 4-row item buffer         // largest node degree with an unrolled fast-path body
 constexpr int kShards = 64;       // early-stop flag words per iteration (one wave load)
 constexpr int kLdsBytes = 160 * 1024;
@@ -200,10 +199,6 @@ struct FlFusedArgs {
   double llr_max;
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, ldb, B, imax, out_dtype, aligned, ngroups;
   int32_t slot16;           // 1: vn_slot staged into LDS as 16-bit indices (after 4 counter words)
-  // variable-update tasks ({first position, count | half << 16, degree, first vn_slot index}): the heavy
-  // degrees' tasks split into two half-slot tasks (half 1 / 2: codewords 0-1 / 2-3 of a 4-codeword slot)
-  const int32_t* vn_utask;
-  int32_t n_vn_utasks;
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED, -DIBL_FUSED_TRACE=1 builds): block 0's clock at
                             // every phase end of its first group, else nullptr
 };

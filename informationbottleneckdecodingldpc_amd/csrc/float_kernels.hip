@@ -678,9 +678,6 @@ __global__ void fl_send(FlArgs a) {
 }
 
 // ------------------------------------------------------------ fused on-chip decoder
-#ifndef IBL_FUSED_STATIC1
-#define IBL_FUSED_STATIC1 1
-#endif
 // For codes whose messages fit in LDS ((E + N) * 16 B <= 160 KiB, e.g. WLAN N=1944: 142.6 KB), one
 // workgroup decodes Vec<F>::N codewords (4 fp32 / 2 fp64, one 16-byte slot per edge and per
 // variable) through ALL iterations without touching HBM: the flooding schedule of
@@ -779,9 +776,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     L = __builtin_amdgcn_readfirstlane(*a.dL);
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
-  // phase tickets start after the waves' static first tasks (see phase)
-  const int wpb = fl_bdim() >> 6;
-  if (fl_tid() < 2) ctr[fl_tid()] = IBL_FUSED_STATIC1 ? wpb : 0;
+  if (fl_tid() < 2) ctr[fl_tid()] = 0;
   SlotIdx vs{nullptr, a.vn_slot};
   if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
     uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
@@ -823,26 +818,9 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       }
     }
   };
-  // variable update: heavy-degree tasks come as two half-slot tasks (vn_utask), so the phase's longest
-  // bodies (WLAN's degree-11 variables: 64 order-preserving sums of 4 codewords per lane) are spread over
-  // twice the waves instead of setting the phase's length
   auto vn_task = [&](int t) __attribute__((always_inline)) {
-    const int pos = sload(a.vn_utask, 4 * t), rec = sload(a.vn_utask, 4 * t + 1);
-    const int d = sload(a.vn_utask, 4 * t + 2), sf = sload(a.vn_utask, 4 * t + 3);
-    const int cnt = rec & 0xFFFF, half = rec >> 16;
-    if constexpr (N == 4) {
-      if (half) {
-        if (lane < cnt) {
-          switch (d) {
-#define X(D) case D: if constexpr (D >= kFlSplitD && D <= VMAX) fused_vn_item<F, D, 2>(msg, chL, vs, pos + lane, sf, cnt, lane, half - 1, lm); break;
-            FL_DEG_CASES(X)
-#undef X
-            default: break;
-          }
-        }
-        return;
-      }
-    }
+    const int pos = sload(a.vn_task, 4 * t), cnt = sload(a.vn_task, 4 * t + 1);
+    const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
     if (lane < cnt) {
       switch (d) {
         case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
@@ -899,15 +877,12 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   };
 
   // ---- phases separated by barriers
-  // A wave's first task of a phase is its wave index (no ticket: the LDS atomic's round trip, with 16
-  // waves on one counter, was on every phase's critical path — C3 runs one check task per wave); further
-  // tasks come from the phase's ticket counter, which starts at the wave count.
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
     int* c = ctr + (ph & 1);
-    if (fl_tid() == 0) ctr[(ph + 1) & 1] = IBL_FUSED_STATIC1 ? wpb : 0;
+    if (fl_tid() == 0) ctr[(ph + 1) & 1] = 0;
     int taken = 0;
     for (;;) {
-      const int t = (IBL_FUSED_STATIC1 && taken == 0) ? wv : take_ticket(c, lane);
+      const int t = take_ticket(c, lane);
       if (t >= ntasks) break;
       if constexpr (IBL_FUSED_TRACE) {
         if (tr && taken == 0) tr[TW * ph + 33 + wv] = __builtin_readcyclecounter();
@@ -940,7 +915,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       phase(a.n_cn_tasks, [&](int t) __attribute__((always_inline)) { cn_task(t, valid, do_par, unsat); });
       if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&a.unsat[(size_t)(j - 1) * kShards + shard], 1);
       if (j == L) break;
-      phase(a.n_vn_utasks, [&](int t) __attribute__((always_inline)) { vn_task(t); });
+      phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { vn_task(t); });
     }
     phase(a.n_vn_tasks, [&](int t) __attribute__((always_inline)) { out_task(t, cw0, valid); });
     tr = nullptr;   // trace the first group only

@@ -50,10 +50,8 @@ VARIANTS = {
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
     "ieeeon": [],
-    # min-sum check node with the (min, second min) pair for every degree; fused kernels' first task per
-    # wave from a ticket like the rest (the round-3 forms)
+    # min-sum check node with the (min, second min) pair for every degree (the round-3 form)
     "msps0": ["IBL_MS_PS=0"],
-    "st0": ["IBL_FUSED_STATIC1=0"],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
