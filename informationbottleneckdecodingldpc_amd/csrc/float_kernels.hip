@@ -678,6 +678,10 @@ __global__ void fl_send(FlArgs a) {
 }
 
 // ------------------------------------------------------------ fused on-chip decoder
+// IBL_FL_CN64: full check tasks (64 nodes) run a body with the constant edge stride (A/B: 0 = off)
+#ifndef IBL_FL_CN64
+#define IBL_FL_CN64 1
+#endif
 // For codes whose messages fit in LDS ((E + N) * 16 B <= 160 KiB, e.g. WLAN N=1944: 142.6 KB), one
 // workgroup decodes Vec<F>::N codewords (4 fp32 / 2 fp64, one 16-byte slot per edge and per
 // variable) through ALL iterations without touching HBM: the flooding schedule of
@@ -717,9 +721,12 @@ __device__ __forceinline__ void slice_store(void* base, int slot, int h, const F
   reinterpret_cast<typename Slice<F, NC>::T*>(base)[slot * (Vec<F>::N / NC) + h] = r;
 }
 
-template <int KIND, typename F, int D, int NC>
-__device__ __forceinline__ void fused_cn_item(void* msg, int first, int cnt, int lane, int h, F lm,
+template <int KIND, typename F, int D, int NC, int CNT = 0>
+__device__ __forceinline__ void fused_cn_item(void* msg, int first, int cnt_, int lane, int h, F lm,
                                               bool do_par, int valid, bool& unsat) {
+  // CNT > 0: a full task (CNT nodes) — the edge stride is a constant, so one address register serves all
+  // D loads and stores through their immediate offsets
+  const int cnt = CNT > 0 ? CNT : cnt_;
   F m[D][NC];
 #pragma unroll
   for (int j = 0; j < D; ++j) slice_load<F, NC>(msg, first + j * cnt + lane, h, m[j]);
@@ -809,7 +816,14 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   };
   auto cn_task = [&](int t, int valid, bool do_par, bool& unsat) __attribute__((always_inline)) {
     const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
-    if (lane < cnt) {
+    if (IBL_FL_CN64 && cnt == 64) {
+      switch (d) {
+#define X(D) case D: if constexpr (D <= CMAX && D <= 8) fused_cn_item<KIND, F, D, NCs, 64>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
+        FL_DEG_CASES(X)
+#undef X
+        default: break;
+      }
+    } else if (lane < cnt) {
       switch (d) {
 #define X(D) case D: if constexpr (D <= CMAX) fused_cn_item<KIND, F, D, NCs>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
         FL_DEG_CASES(X)

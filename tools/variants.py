@@ -52,6 +52,8 @@ VARIANTS = {
     "ieeeon": [],
     # min-sum check node with the (min, second min) pair for every degree (the round-3 form)
     "msps0": ["IBL_MS_PS=0"],
+    # fused float check tasks without the constant-stride body for full tasks
+    "cn64off": ["IBL_FL_CN64=0"],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
