@@ -187,7 +187,7 @@ struct ibl_float {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
-  int32_t f_ncn = 0, f_nvn = 0, f_slot16 = 0;
+  int32_t f_ncn = 0, f_nvn = 0, f_nvs = 0;
   size_t f_lds = 0;
   int f_grid = 0;
 };
@@ -813,36 +813,41 @@ int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_tas
 int fused_setup(ibl_float* h) {
   const ibl_graph* g = h->g;
   const int64_t E = g->n_e;
-  size_t lds = (size_t)(E + g->n_v) * 16 + 16;
-  // variable-edge slot indices as u16 in LDS when they fit (E < 65536 and the space is there)
-  const size_t lds16 = (size_t)(E + g->n_v) * 16 + 16 + (size_t)E * 2;
-  // IBL_FUSED_SLOT16=0 forces the global int32 slot reads (test hook: tests/test_gpu_float.py runs that path)
-  const char* s16e = getenv("IBL_FUSED_SLOT16");
-  const bool slot16 = E < 65536 && lds16 <= (size_t)kLdsBytes && !(s16e && s16e[0] == '0');
-  if (slot16) lds = lds16;
   int min_dc = 1 << 30;
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
-  if (lds > (size_t)kLdsBytes || min_dc < 2 || E == 0) return IBL_OK;
-  int bpc = 0, block = 0;
-  if (fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lds, &bpc, &block) != hipSuccess || bpc < 1) {
-    (void)hipGetLastError();
-    return IBL_OK;
-  }
+  if (E >= 65536 || min_dc < 2 || E == 0 || (size_t)(E + g->n_v) * 16 > (size_t)kLdsBytes) return IBL_OK;
   FusedTasks ft;
   int rc;
   // 16-byte slots (ds_read_b128 / ds_write_b128): the natural order (stable by degree) keeps a quasi-cyclic
   // code's lanes on runs of consecutive slots, which conflict less than the dword-bank greedy order;
   // IBL_FUSED_VORDER=1 selects the greedy order (A/B)
   const char* voe = getenv("IBL_FUSED_VORDER");
-  if ((rc = build_fused_tasks(g, &ft, voe && voe[0] == '1')) ||
-      (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
-    return rc;
-  const std::vector<int32_t>& cn_task = ft.cn_task;
-  const std::vector<int32_t>& vn_task = ft.vn_task;
-  h->f_ncn = (int32_t)(cn_task.size() / 4);
-  h->f_nvn = (int32_t)(vn_task.size() / 4);
+  if ((rc = build_fused_tasks(g, &ft, voe && voe[0] == '1'))) return rc;
+  // The kernel keeps the variable-edge slot indices in LDS as u16, each variable task's rows at the full
+  // stride of 64 lanes (record field 3 = the task's first padded index): the D index loads of a task share
+  // one address and take their row offsets as immediates, whatever the task's node count.
+  std::vector<int32_t> pslot;
+  for (size_t t = 0; t < ft.vn_task.size() / 4; ++t) {
+    const int32_t cnt = ft.vn_task[4 * t + 1], d = ft.vn_task[4 * t + 2], sf = ft.vn_task[4 * t + 3];
+    ft.vn_task[4 * t + 3] = (int32_t)pslot.size();
+    for (int32_t k = 0; k < d; ++k)
+      for (int32_t i = 0; i < 64; ++i) pslot.push_back(i < cnt ? ft.vn_slot[sf + (size_t)k * cnt + i] : 0);
+  }
+  ft.vn_slot.swap(pslot);
+  // messages and channel (16-byte slots), 4 counter words, the padded u16 indices (codes whose indices do
+  // not fit beside the messages take the per-pass path)
+  const size_t lds = (size_t)(E + g->n_v) * 16 + 16 + ft.vn_slot.size() * 2;
+  if (lds > (size_t)kLdsBytes) return IBL_OK;
+  int bpc = 0, block = 0;
+  if (fl_fused_occupancy(h->kind, h->prec, g->dcm, g->dvm, lds, &bpc, &block) != hipSuccess || bpc < 1) {
+    (void)hipGetLastError();
+    return IBL_OK;
+  }
+  if ((rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot))) return rc;
+  h->f_ncn = (int32_t)(ft.cn_task.size() / 4);
+  h->f_nvn = (int32_t)(ft.vn_task.size() / 4);
+  h->f_nvs = (int32_t)ft.vn_slot.size();
   h->f_lds = lds;
-  h->f_slot16 = slot16 ? 1 : 0;
   h->f_grid = bpc * g->num_cus;
   h->fused_ok = true;
   return IBL_OK;
@@ -1098,9 +1103,8 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.ch = h->chf; fa.cn_task = h->f_cn_task; fa.vn_task = h->f_vn_task; fa.vn_node = h->f_vn_node;
     fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
     fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
-    fa.n_vn_tasks = h->f_nvn; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
+    fa.n_vn_tasks = h->f_nvn; fa.n_vs = h->f_nvs; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
     fa.ngroups = (B + cwl - 1) / cwl;
-    fa.slot16 = h->f_slot16;
     const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
     const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {

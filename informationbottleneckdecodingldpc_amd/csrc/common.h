@@ -192,13 +192,13 @@ struct FlFusedArgs {
   const int32_t* cn_task;   // per check task: {first slot, count, degree, 0}
   const int32_t* vn_task;   // per variable task: {first position, count, degree, first vn_slot index}
   const int32_t* vn_node;   // variable position -> node
-  const int32_t* vn_slot;   // variable task edge k, lane i at [first + k*count + i] -> message slot
+  const int32_t* vn_slot;   // variable task edge k, lane i at [first + 64k + i] -> message slot
   void* out;                // user output [N][B] (out_dtype)
   int32_t* unsat;           // non-null: CN pass j ORs "unsatisfied" into unsat[(j-1)*kShards + shard]
   const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
   double llr_max;
   int32_t n_e, n_v, n_cn_tasks, n_vn_tasks, ldb, B, imax, out_dtype, aligned, ngroups;
-  int32_t slot16;           // 1: vn_slot staged into LDS as 16-bit indices (after 4 counter words)
+  int32_t n_vs;             // variable-edge slot indices (vn_slot), each task's rows padded to 64 lanes
   uint64_t* trace;          // diagnostics (IBL_TRACE_FUSED, -DIBL_FUSED_TRACE=1 builds): block 0's clock at
                             // every phase end of its first group, else nullptr
 };

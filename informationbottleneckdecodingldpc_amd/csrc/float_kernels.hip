@@ -739,20 +739,15 @@ __device__ __forceinline__ void fused_cn_item(void* msg, int first, int cnt_, in
   });
 }
 
-// Variable-edge slot indices: staged into LDS as 16-bit values when they fit beside the messages (one
-// LDS read instead of an L2 round trip per variable task and phase), else read from global memory.
-struct SlotIdx {
-  const uint16_t* s16;   // LDS copy, or nullptr
-  const int32_t* s32;    // global array
-  __device__ __forceinline__ int operator[](int i) const { return s16 ? (int)s16[i] : s32[i]; }
-};
-
+// Variable-edge slot indices: staged into LDS as 16-bit values beside the messages (the fused path
+// requires the room for them, capi.hip fused_setup), row k of a task at sfirst + 64k: the D loads share
+// one address and take their row offsets as immediates.
 template <typename F, int D, int NC>
-__device__ __forceinline__ void fused_vn_item(void* msg, const void* chL, const SlotIdx& vn_slot, int pos,
-                                              int sfirst, int cnt, int lane, int h, F lm) {
+__device__ __forceinline__ void fused_vn_item(void* msg, const void* chL, const uint16_t* vn_slot, int pos,
+                                              int sfirst, int lane, int h, F lm) {
   int sl[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) sl[k] = vn_slot[sfirst + k * cnt + lane];
+  for (int k = 0; k < D; ++k) sl[k] = vn_slot[sfirst + 64 * k + lane];
   F c[NC], m[D][NC];
   slice_load<F, NC>(chL, pos, h, c);
 #pragma unroll
@@ -784,12 +779,9 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
   if (fl_tid() < 2) ctr[fl_tid()] = 0;
-  SlotIdx vs{nullptr, a.vn_slot};
-  if (a.slot16) {   // [ctr x 4][E x u16] after the channel slots
-    uint16_t* s16 = reinterpret_cast<uint16_t*>(ctr + 4);
-    for (int i = fl_tid(); i < a.n_e; i += fl_bdim()) s16[i] = (uint16_t)a.vn_slot[i];
-    vs.s16 = s16;
-  }
+  // variable-edge slot indices, [ctr x 4][n_vs x u16] after the channel slots
+  uint16_t* vs = reinterpret_cast<uint16_t*>(ctr + 4);
+  for (int i = fl_tid(); i < a.n_vs; i += fl_bdim()) vs[i] = (uint16_t)a.vn_slot[i];
   __syncthreads();
   int ph = 0;
   const int shard = (int)((fl_bid() * (fl_bdim() >> 6) + (fl_tid() >> 6)) & (kShards - 1));
@@ -811,7 +803,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       // channel staged as [group][variable position] (fl_stage_t): a task reads consecutive slots
       const VT c = reinterpret_cast<const VT*>(a.ch)[(size_t)grp * a.n_v + pos + lane];
       chL[pos + lane] = c;
-      for (int k = 0; k < d; ++k) msg[vs[sf + k * cnt + lane]] = c;
+      for (int k = 0; k < d; ++k) msg[vs[sf + 64 * k + lane]] = c;
     }
   };
   auto cn_task = [&](int t, int valid, bool do_par, bool& unsat) __attribute__((always_inline)) {
@@ -837,8 +829,8 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     const int d = sload(a.vn_task, 4 * t + 2), sf = sload(a.vn_task, 4 * t + 3);
     if (lane < cnt) {
       switch (d) {
-        case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
-#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, cnt, lane, h, lm); break;
+        case 1: fused_vn_item<F, 1, NCs>(msg, chL, vs, pos + lane, sf, lane, h, lm); break;
+#define X(D) case D: if constexpr (D <= VMAX) fused_vn_item<F, D, NCs>(msg, chL, vs, pos + lane, sf, lane, h, lm); break;
         FL_DEG_CASES(X)
 #undef X
         default: break;
@@ -859,7 +851,7 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
       }
       if (L > 0)
         for (int k = 0; k < d; ++k) {
-          const VT r = msg[vs[sf + k * cnt + lane]];
+          const VT r = msg[vs[sf + 64 * k + lane]];
 #pragma unroll
           for (int s = 0; s < N; ++s) x[s] = x[s] + V::get(r, s);
         }

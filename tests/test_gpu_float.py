@@ -338,21 +338,6 @@ def test_float32_minsum_tiny_llrs(eng, wlan_H, path):
     np.testing.assert_array_equal(out, ref.astype(np.float64))
 
 
-@pytest.mark.parametrize("prec", [torch.float32, torch.float64])
-def test_fused_global_slot_index_path(eng, monkeypatch, wlan_H, prec):
-    """The fused float kernel's fallback that reads variable-edge slot indices from global memory (taken when
-    the u16 copy does not fit in LDS; IBL_FUSED_SLOT16=0 forces it at create) equals the per-pass path."""
-    g = graph.build_graph(wlan_H)
-    G = eng.Graph(g, DEV)
-    llr = _llrs(g, 130, 2.0, seed=29)
-    monkeypatch.setenv("IBL_FUSED_SLOT16", "0")
-    fused, it_f = _gpu(eng, g, oracle.MINSUM, 12, llr, prec, True, graph_obj=G, path="fused")
-    monkeypatch.delenv("IBL_FUSED_SLOT16")
-    passes, it_p = _gpu(eng, g, oracle.MINSUM, 12, llr, prec, True, graph_obj=G, path="passes")
-    assert it_f == it_p
-    np.testing.assert_array_equal(fused, passes)
-
-
 @pytest.mark.parametrize("prec,kind", [(torch.float32, oracle.MINSUM), (torch.float64, oracle.MINSUM)])
 @pytest.mark.parametrize("path", ["auto", "passes"])
 def test_float_infinite_channel_llrs(eng, wlan_H, prec, kind, path):
