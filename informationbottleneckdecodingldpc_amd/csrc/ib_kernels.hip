@@ -1017,8 +1017,13 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     // send: the channel value to every edge slot of its variable
     mark(0);
     pf.load(a.cn_img, a.cn_nt);
+    // (the slot indices are the task's prefetched ones: re-reading them from global memory here put an
+    // unprefetched L2 round trip in every task — C1's send phase took 22k cycles against 15k for an
+    // iteration's phase)
     vn_phase(chg, csh, [&](const VnTask<MAXD>& v) __attribute__((always_inline)) {
-      for (int k = 0; k < v.d; ++k) msg[a.vn_slot[v.sf + k * v.cnt + lane]] = v.chw;
+#pragma unroll
+      for (int k = 0; k < MAXD; ++k)
+        if (k < v.d) msg[v.sl[k]] = v.chw;
     });
     next_phase();
     for (int j = 0;; ++j) {
