@@ -11,6 +11,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -40,7 +41,7 @@ def run(name, steps, warmup):
     ms = e0.elapsed_time(e1) / steps
     # every codeword satisfies H x = 0 (checked on the last step's output)
     Hc = H.tocoo()
-    Hd = torch.sparse_coo_tensor(torch.tensor([Hc.row, Hc.col], dtype=torch.long), torch.ones(Hc.nnz),
+    Hd = torch.sparse_coo_tensor(torch.from_numpy(np.stack([Hc.row, Hc.col]).astype(np.int64)), torch.ones(Hc.nnz),
                                  Hc.shape).to(dev)
     syn = torch.remainder(torch.sparse.mm(Hd, out[:, :64].float()), 2).abs().sum().item()
     bpc = enc.K + enc.N
