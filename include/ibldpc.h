@@ -152,8 +152,10 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
 void ibl_float_destroy(ibl_float* h);
 /*
  * Decode path of a float decoder (no reference counterpart; results are identical on both):
- *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits in LDS
- *                            ((E + N) * 16 bytes <= 160 KiB, check degrees >= 2), else IBL_PATH_PASSES;
+ *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits in LDS ((E + N) * 16 bytes of
+ *                            messages and channel plus 2 bytes per variable edge slot index — each
+ *                            variable task's rows padded to 64 — within 160 KiB, E < 65536, check
+ *                            degrees >= 2), else IBL_PATH_PASSES;
  *   IBL_PATH_PASSES          one launch per check / variable pass, messages in HBM;
  *   IBL_PATH_FUSED           the fused kernel (IBL_EUNSUPPORTED if the code does not fit).
  * ibl_float_path_in_use reports 1 when decodes run the fused kernel, 0 otherwise.  With the fused
