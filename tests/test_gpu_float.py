@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 import torch
 
-from informationbottleneckdecodingldpc_amd import graph
+from informationbottleneckdecodingldpc_amd import codes, graph
 from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
 from oracle import oracle
 from tests._codes import mixed_code
@@ -320,6 +320,15 @@ def test_fused_path_selection(eng, wlan_H, dvb_H):
     from informationbottleneckdecodingldpc_amd._lib import IBLError
     with pytest.raises(IBLError):
         eng.FloatDecoder(D, 0, 5, 16, path="fused")
+    # the fused kernel keeps the variable-edge slot indices in LDS too (u16, task rows padded to 64):
+    # regular (3,6) N=2304: 64 N + 16 + 6 N = 161,296 B fits; N=2400: the messages alone (153,616 B) would,
+    # with the indices (168,016 B) they do not -> the per-pass path
+    for n, fits in ((2304, True), (2400, False)):
+        R = eng.Graph(graph.build_graph(codes.regular_code(n, 3, 6, seed=1)), DEV)
+        assert eng.FloatDecoder(R, 0, 5, 16).fused == fits
+        if not fits:
+            with pytest.raises(IBLError):
+                eng.FloatDecoder(R, 0, 5, 16, path="fused")
 
 
 @pytest.mark.parametrize("path", ["auto", "passes"])
