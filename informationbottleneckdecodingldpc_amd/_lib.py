@@ -29,7 +29,7 @@ EXPORTS = [
     "ibl_ib_create", "ibl_ib_path", "ibl_ib_set_path", "ibl_ib_path_in_use", "ibl_ib_fused_ncw", "ibl_ib_decode",
     "ibl_ib_destroy",
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
-    "ibl_float_set_path", "ibl_float_path_in_use", 
+    "ibl_float_set_path", "ibl_float_path_in_use",
     "ibl_ib_timing", "ibl_ib_timing_read", "ibl_float_timing", "ibl_float_timing_read",
     "ibl_channel_sample",
     "ibl_encoder_create",

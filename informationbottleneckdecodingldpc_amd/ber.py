@@ -232,7 +232,16 @@ def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: in
 def _drive(gens, exchange):
     """Run rank generators in lockstep: each round's local counts go through ``exchange`` (a list of the
     gens' lists -> the [world][k] matrix) and the matrix is sent back to every gen."""
-    locals_ = [next(g) for g in gens]
+    locals_, done = [], []
+    for g in gens:      # a sweep that decodes nothing (min_errors <= 0, max_blocks <= 0) returns before a yield
+        try:
+            locals_.append(next(g))
+        except StopIteration as e:
+            done.append(e.value)
+    if done:
+        if len(done) != len(gens):
+            raise RuntimeError("ranks of a BER sweep disagree on when to stop")
+        return done
     while True:
         counts = exchange(locals_)
         nxt, done = [], []

@@ -21,6 +21,12 @@
 
 using namespace ibl;
 
+// IBL_DIAG=1 (diagnostic builds, tools/variants.py): the timing-only hooks IBL_VN_PART, IBL_TRACE_WAVES and
+// IBL_TRACE_FUSED. The product build has none of them: no decode call reads the environment.
+#ifndef IBL_DIAG
+#define IBL_DIAG 0
+#endif
+
 static thread_local std::string g_err;
 static inline void dfree(void* p) {
   if (p) (void)hipFree(p);
@@ -30,14 +36,18 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-// IBL_DEBUG_SYNC=1: synchronise after every launch so an asynchronous fault is reported at the
-// launch that caused it (debugging only; breaks the no-host-sync property of decode).
+// Diagnostic builds: IBL_DEBUG_SYNC=1 synchronises after every launch so an asynchronous fault is
+// reported at the launch that caused it (breaks the no-host-sync property of decode).
 static bool debug_sync() {
+#if IBL_DIAG
   static const bool on = [] {
     const char* v = getenv("IBL_DEBUG_SYNC");
     return v && *v && *v != '0';
   }();
   return on;
+#else
+  return false;
+#endif
 }
 #define HIPCHK(expr)                                                                        \
   do {                                                                                      \
@@ -166,6 +176,7 @@ struct ibl_ib {
   // fused on-chip path (IbFusedArgs, short codes): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false, f_half_ok = false;   // f_half_ok: the 4-codeword-group kernel is usable too
+  int32_t f_ncw_forced = 0;                   // IBL_FUSED_NCW read once at create (A/B, tests), 0 = auto
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
@@ -374,11 +385,11 @@ bool ib_fused_in_use(const ibl_ib* h);
 // doubled number of workgroups fits the grid (each half group then has a workgroup slot of its own);
 // whole 8-codeword groups otherwise — with 2*ngroups > grid some workgroups would run two half groups in
 // a row, and a half group takes more than half a group's time (per-phase latency). The
-// environment IBL_FUSED_NCW=8 / 4 forces either (A/B, tests); 4 needs the half-group kernel (f_half_ok).
+// environment IBL_FUSED_NCW=8 / 4, read once when the decoder is created, forces either (A/B, tests); 4
+// needs the half-group kernel (f_half_ok).
 int ib_fused_ncw(const ibl_ib* h, int B) {
   const int ngroups = (B + 7) / 8;
-  const char* e = getenv("IBL_FUSED_NCW");
-  const int forced = e ? atoi(e) : 0;
+  const int forced = h->f_ncw_forced;
   if (!h->f_half_ok || forced == 8) return 8;
   return (forced == 4 || 2 * ngroups <= h->f_grid) ? 4 : 8;
 }
@@ -650,14 +661,18 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     f.ngroups = (B + 7) / 8;
     f.ncw = ib_fused_ncw(h, B);
     const int grid = std::min(h->f_grid, f.ngroups * (8 / f.ncw));
-    // diagnostics: IBL_TRACE_FUSED=<file> records block 0's clock at every phase boundary of its first group
+#if IBL_DIAG
+    // diagnostic builds only: IBL_TRACE_FUSED=<file> records block 0's clock at every phase boundary of its
+    // first group (with -DIBL_FUSED_TRACE=1 kernels, tools/variants.py ftrace)
     const char* ftrace = getenv("IBL_TRACE_FUSED");
     const size_t ntr = (size_t)3 * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&f.trace, sizeof(uint64_t) * ntr));
       HIPCHK(hipMemsetAsync(f.trace, 0, sizeof(uint64_t) * ntr, s));
     }
+#endif
     HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_fused(f, h->CM, h->VM, grid, h->f_block, h->f_lds, s); }));
+#if IBL_DIAG
     if (ftrace) {
       std::vector<uint64_t> hv(ntr);
       HIPCHK(hipStreamSynchronize(s));
@@ -669,6 +684,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
         fclose(fp);
       }
     }
+#endif
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     if (early) {   // pass 2: re-run the batch to the stop iteration (a no-op when it is imax-1)
       f.unsat = nullptr;
@@ -687,7 +703,8 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     vn.info = g->vn_info; vn.tgt = g->tgt_vn; vn.out = h->cin; vn.in = h->vin;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
     cn.n_heavy = g->cn_heavy; vn.n_heavy = g->vn_heavy;
-    // diagnostics (timing only, outputs are not decodes): IBL_VN_PART=heavy / light runs the variable
+#if IBL_DIAG
+    // diagnostic builds only (timing, outputs are not decodes): IBL_VN_PART=heavy / light runs the variable
     // pass over one item class only (the degree > kLightD items, or the rest)
     if (const char* vp = getenv("IBL_VN_PART")) {
       if (vp[0] == 'h') {
@@ -698,6 +715,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
         vn.n_heavy = 0;
       }
     }
+#endif
     cn.nchunks = (B + ccn - 1) / ccn;
     vn.nchunks = (B + cvn - 1) / cvn;
     cn.ldb = vn.ldb = ldbb;
@@ -716,12 +734,16 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     auto launch_cn = [&]() { return launch_ib_cn_fast(cn, h->CM, h->kcn.grid, h->kcn.block, h->kcn.lds, s); };
     HIPCHK(h->timer.timed(0, s, launch_cn));
     cn.gather = nullptr;
-    // diagnostics: IBL_TRACE_WAVES=<prefix> records {start, end, items|cu} of every wave of the middle
-    // iteration's VN and CN launches into <prefix>_vn.bin / <prefix>_cn.bin (uint64 triples)
-    const char* trace_path = getenv("IBL_TRACE_WAVES");
     uint64_t* trace = nullptr;
+#if IBL_DIAG
+    // diagnostic builds only: IBL_TRACE_WAVES=<prefix> records {start, end, items|cu} of every wave of the
+    // middle iteration's VN and CN launches into <prefix>_vn.bin / <prefix>_cn.bin (uint64 triples)
+    const char* trace_path = getenv("IBL_TRACE_WAVES");
     const size_t nwv = (size_t)h->kvn.grid * (h->kvn.block / 64), nwc = (size_t)h->kcn.grid * (h->kcn.block / 64);
     if (trace_path && I > 1) HIPCHK(hipMalloc((void**)&trace, sizeof(uint64_t) * 3 * (nwv + nwc)));
+#else
+    const size_t nwv = 0;
+#endif
     for (int j = 1; j < I; ++j) {
       const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
       vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
@@ -737,6 +759,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
       cn.in = h->cin;
       HIPCHK(h->timer.timed(0, s, launch_cn));
     }
+#if IBL_DIAG
     if (trace) {
       std::vector<uint64_t> hv(3 * (nwv + nwc));
       HIPCHK(hipStreamSynchronize(s));
@@ -750,6 +773,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
         }
       }
     }
+#endif
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     IbDecArgs dc{};
     dc.vin = h->vin; dc.ch8 = h->ch8; dc.start = g->vn_start; dc.deg = g->vn_deg; dc.img = h->dec_img;
@@ -997,6 +1021,7 @@ int ib_fused_setup(ibl_ib* h) {
     h->f_cn_uni = uniform(ft.cn_task, g->n_c, false);
     h->f_vn_uni = uniform(ft.vn_task, g->n_v, true);
   }
+  if (const char* ne = getenv("IBL_FUSED_NCW")) h->f_ncw_forced = atoi(ne);
   h->f_nreg = nreg;
   h->f_dbuf = dbuf ? 1 : 0;
   h->f_lds = lds;
@@ -1105,16 +1130,19 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     fa.llr_max = h->llr_max; fa.n_e = (int32_t)g->n_e; fa.n_v = g->n_v; fa.n_cn_tasks = h->f_ncn;
     fa.n_vn_tasks = h->f_nvn; fa.n_vs = h->f_nvs; fa.ldb = h->ldb; fa.B = B; fa.imax = I; fa.out_dtype = out_dtype;
     fa.ngroups = (B + cwl - 1) / cwl;
-    const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostics: phase clocks of block 0's first group
+#if IBL_DIAG
+    const char* ftrace = getenv("IBL_TRACE_FUSED");   // diagnostic builds: phase clocks of block 0's first group
     const size_t ntr = (size_t)kFlTraceWords * (2 * I + 4);
     if (ftrace) {
       HIPCHK(hipMalloc((void**)&fa.trace, sizeof(uint64_t) * ntr));
       HIPCHK(hipMemsetAsync(fa.trace, 0, sizeof(uint64_t) * ntr, s));
     }
+#endif
     const size_t esz = out_dtype == kF32 ? 4 : 8;
     fa.aligned = ((B % cwl) == 0 && ((uintptr_t)d_out % (cwl * esz)) == 0) ? 1 : 0;
     const int grid = std::min(fa.ngroups, h->f_grid);
     HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_fused(fa, h->kind, h->prec, g->dcm, g->dvm, grid, h->f_lds, s); }));
+#if IBL_DIAG
     if (ftrace) {
       std::vector<uint64_t> hv(ntr);
       HIPCHK(hipStreamSynchronize(s));
@@ -1126,6 +1154,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
         fclose(fp);
       }
     }
+#endif
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     if (early) {   // batch-global stop before imax-1: re-run the batch to L (the kernel exits if L = imax-1)
       fa.unsat = nullptr;

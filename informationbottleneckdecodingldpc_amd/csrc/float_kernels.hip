@@ -808,7 +808,9 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
   };
   auto cn_task = [&](int t, int valid, bool do_par, bool& unsat) __attribute__((always_inline)) {
     const int first = sload(a.cn_task, 4 * t), cnt = sload(a.cn_task, 4 * t + 1), d = sload(a.cn_task, 4 * t + 2);
-    if (IBL_FL_CN64 && cnt == 64) {
+    // the constant-stride body exists for degrees <= 8 only; full tasks of larger degrees take the general
+    // branch below (every lane < cnt = 64)
+    if (IBL_FL_CN64 && cnt == 64 && d <= 8) {
       switch (d) {
 #define X(D) case D: if constexpr (D <= CMAX && D <= 8) fused_cn_item<KIND, F, D, NCs, 64>(msg, first, cnt, lane, h, lm, do_par, valid, unsat); break;
         FL_DEG_CASES(X)

@@ -211,6 +211,18 @@ def test_ber_sweep_is_world_size_invariant(world, sync):
     np.testing.assert_array_equal(many.EbN0_dB_vector, one.EbN0_dB_vector)
 
 
+@pytest.mark.parametrize("kw", [dict(min_errors=0), dict(max_blocks=0)])
+def test_ber_sweep_that_decodes_nothing(kw):
+    """A sweep whose stop rule holds before the first batch (the rank generator returned before
+    its first yield and run_ber raised a bare StopIteration) gives one zero-block point, on 1 and 3 ranks."""
+    cfg = BERConfig(**{**_SWEEP, **kw})
+    one = run_ber(_GlobalIB(None), cfg, quantizer_factory=_GlobalQuanti)
+    assert one.blocks == [0] and one.errors == [0.0]
+    np.testing.assert_array_equal(one.BER_vector, [0.0])
+    many = ber.run_ber_lockstep(_GlobalIB(None), cfg, 3, quantizer_factory=_GlobalQuanti)
+    assert many.blocks == [0] and many.errors == [0.0]
+
+
 def test_ber_world_override_needs_process_group():
     with pytest.raises(ValueError, match="run_ber_lockstep"):
         run_ber(_GlobalIB(None), BERConfig(**_SWEEP), quantizer_factory=_GlobalQuanti, world=2)

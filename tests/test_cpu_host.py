@@ -38,6 +38,28 @@ def test_library_exports_every_header_symbol(lib):
     assert L.ibl_version() == 3
 
 
+def test_product_library_has_no_diagnostic_hooks(lib):
+    """The timing-only hooks (IBL_VN_PART runs part of the variable pass: its outputs are not decodes;
+    IBL_TRACE_WAVES / IBL_TRACE_FUSED allocate and sync per decode; IBL_DEBUG_SYNC syncs per launch) exist
+    only in diagnostic builds (-DIBL_DIAG=1, tools/variants.py diag / ftrace): the product library does not
+    even hold their names, so no environment variable can change what a decode computes or costs. The
+    create-time A/B knobs stay (read once per decoder)."""
+    from informationbottleneckdecodingldpc_amd import _build
+    _build.build()
+    blob = open(lib.LIB_PATH, "rb").read()
+    for name in (b"IBL_VN_PART", b"IBL_TRACE_WAVES", b"IBL_TRACE_FUSED", b"IBL_DEBUG_SYNC"):
+        assert name not in blob, name
+    src = open(os.path.join(ROOT, "informationbottleneckdecodingldpc_amd", "csrc", "capi.hip")).read()
+    # every getenv outside the diagnostic blocks sits in a create-time function
+    body = re.sub(r"#if IBL_DIAG.*?#endif", "", src, flags=re.S)
+    decode_fns = re.findall(r"\nint (ibl_(?:ib|float)_decode)\(.*?\n}\n", body, flags=re.S)
+    assert len(decode_fns) == 2
+    for m in re.finditer(r"\nint (ibl_(?:ib|float)_decode)\(.*?\n}\n", body, flags=re.S):
+        assert "getenv" not in m.group(0), m.group(1)
+    ncw = re.search(r"int ib_fused_ncw\(.*?\n}\n", body, flags=re.S).group(0)
+    assert "getenv" not in ncw
+
+
 def test_library_device_count_without_gpu(lib):
     import torch
     if torch.cuda.is_available():

@@ -300,6 +300,28 @@ def test_fused_equals_passes(eng, prec, kind, name, imax, B, early, ebn0, wlan_H
     np.testing.assert_array_equal(fused, passes)
 
 
+@pytest.mark.parametrize("prec", [torch.float32, torch.float64])
+@pytest.mark.parametrize("kind", [oracle.MINSUM, oracle.BP])
+def test_fused_full_tasks_of_check_degree_above_8(eng, prec, kind):
+    """A code with full (64-node) check tasks of degree 10 — the fused kernel's constant-stride body
+    covers degrees <= 8 only, so these tasks must take the general body (they were skipped).
+    Regular (3,10), N=960: 288 checks of degree 10 = 4 full tasks + one of 32. Fused == per-pass, and the
+    fp64 min-sum decode == the oracle."""
+    g = graph.build_graph(codes.regular_code(960, 3, 10, seed=3))
+    assert g.d_c_max == 10 and g.n_c >= 256
+    G = eng.Graph(g, DEV)
+    B, imax = 70, 12
+    llr = _llrs(g, B, 3.0, seed=41, quantised=True)
+    fused, it_f = _gpu(eng, g, kind, imax, llr, prec, True, graph_obj=G, path="fused")
+    passes, it_p = _gpu(eng, g, kind, imax, llr, prec, True, graph_obj=G, path="passes")
+    assert it_f == it_p
+    np.testing.assert_array_equal(fused, passes)
+    if kind == oracle.MINSUM and prec == torch.float64:
+        ref, ref_it = oracle.float_decode(g, kind, imax, llr, early_stop=True, return_iters=True)
+        assert it_f == ref_it
+        np.testing.assert_array_equal(fused, ref)
+
+
 def test_fused_stop_iteration_and_outputs_vs_oracle(eng, wlan_H):
     """Early stop inside the fused path (pass 2) against the fp64 oracle directly."""
     g = graph.build_graph(wlan_H)

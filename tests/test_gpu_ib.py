@@ -35,6 +35,22 @@ def _run(eng, g_edges, tb, ch, match, early, out_dtype=torch.int32, ch_dtype=tor
     return out.cpu().numpy().astype(np.int32), int(it.item()), dec
 
 
+def test_decode_ignores_diagnostic_environment(eng, dvb_H, monkeypatch):
+    """IBL_VN_PART made every per-pass decode skip part of the variable pass. The product
+    library has no such hook any more (diagnostic builds only), so a decode with it set — and with the other
+    timing-only variables set — still equals the oracle."""
+    monkeypatch.setenv("IBL_VN_PART", "heavy")
+    monkeypatch.setenv("IBL_TRACE_WAVES", "/nonexistent/trace")
+    monkeypatch.setenv("IBL_TRACE_FUSED", "/nonexistent/ftrace")
+    g = graph.build_graph(dvb_H)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 4, seed=3)
+    ch = np.random.default_rng(3).integers(0, 16, (g.n_v, 9)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=True, early_stop=False)
+    out, _, dec = _run(eng, g, tb, ch, True, False, path="passes")
+    assert dec.fast_path
+    np.testing.assert_array_equal(out, ref)
+
+
 CASES = [
     # name, imax, B, match, early
     ("wlan", 1, 3, False, False),

@@ -74,7 +74,7 @@ for s in $STEPS; do
         done
       done;;
     trace)   # per-wave clocks of the per-pass IB kernels (tools/wave_balance.py)
-      IBL_TRACE_WAVES=$O/trace timeout -k 10 300 python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.json 2> $O/bench_trace.err
+      IBL_TRACE_WAVES=$O/trace IBLDPC_LIB=$VL/libibldpc_diag.so timeout -k 10 300 python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $O/bench_trace.json 2> $O/bench_trace.err
       chk $? trace; echo "trace ok" >> $O/summary.txt;;
     ftrace)  # fused-kernel phase trace (variant `ftrace`; tools/fused_trace.py, tools/fused_trace_fl.py)
       for c in $CONFIGS; do

@@ -38,9 +38,10 @@ VARIANTS = {
     "w1s8": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1s8.inc"'],
     "w1l4": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1l4.inc"'],
     "w2l4": ['IBL_SCHED_FILE="ib_sched_w2l4.inc"'],
-    "w1": ["IBL_W=1"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
-    "ftrace": ["IBL_FUSED_TRACE=1"],
+    "ftrace": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1"],
+    # timing-only host hooks (IBL_VN_PART, IBL_TRACE_WAVES, IBL_DEBUG_SYNC): not in the product build
+    "diag": ["IBL_DIAG=1"],
     # column fetches (tools/gen_sched.py "Column fetches"; the schedule file is generated on demand).
     # Measured on DVB-S2 (B=8192, i_max=50): nc00 170.9k cw/s (CN 0.464 / VN 0.478 ms), nc23 140.9k
     # (0.622 / 0.526), nc22 142.0k, nc33 132.3k, s2 156.5k -> the default build keeps NC = 0.
