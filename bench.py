@@ -40,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+CH_SEED = 2              # Philox key of the synthetic channel ("seed 2, keyed by global codeword index")
 
 
 def parse():
@@ -49,7 +50,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--batch-per-gpu", type=int, default=8192)
     p.add_argument("--imax", type=int, default=50)
-    p.add_argument("--ebn0", type=float, default=0.6)
+    p.add_argument("--ebn0", type=float, default=None, help="Eb/N0 in dB (default 0.6; 1.0 with --early-stop)")
     p.add_argument("--kind", choices=["ib", "minsum", "bp"], default="ib")
     p.add_argument("--code", choices=["dvbs2", "regular", "wlan"], default="dvbs2")
     p.add_argument("--config", choices=["C1", "C2", "C3", "C4", "C5"], default=None,
@@ -60,14 +61,24 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
     p.add_argument("--cpu-procs", type=int, default=0, help="CPU-baseline processes / oracle threads (0 = this job's CPU share, bench.cpu_share())")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--early-stop", action="store_true",
+                   help="batch-global early stop on (SURVEY §8(d)'s second line: at 1.0 dB unless --ebn0 is given); "
+                        "IB decoders use LLR-derived tables (tables.llr_tables) so the batch can converge")
+    p.add_argument("--batch-offset", type=int, default=0,
+                   help="global batch index of rank 0's batch: rank r decodes global batch offset + r, whose channel "
+                        "is Philox key 2 at counter (offset + r) * philox_blocks(N, B) (SURVEY H9)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     a = p.parse_args()
     presets = {"C1": ("regular", "ib", 10, 1000), "C2": ("regular", "ib", 50, 65536),
                "C3": ("wlan", "minsum", 50, 262144), "C4": ("dvbs2", "ib", 50, 8192), "C5": ("dvbs2", "bp", 100, 8192)}
     if a.config:
-        a.code, a.kind, a.imax, a.batch_per_gpu = presets[a.config]
+        a.code, a.kind, a.imax, B = presets[a.config]
+        if "--batch-per-gpu" not in sys.argv:
+            a.batch_per_gpu = B
         if a.config in ("C1", "C2"):
             a.no_match = True      # Discrete_LDPC_Decoder_class (regular) has no matching step
+    if a.ebn0 is None:
+        a.ebn0 = 1.0 if a.early_stop else 0.6
     return a
 
 
@@ -92,19 +103,29 @@ def bytes_per_cw(n_e: int, n_v: int, imax: int, w: int) -> int:
 
 
 def moved_bytes_per_cw(n_e: int, n_v: int, imax: int, path: str, ws: float, w_in: int, w_out: int,
-                       w_stage: float = 1) -> float:
+                       w_stage: float = 1, folded: int = 0) -> float:
     """HBM bytes one codeword's decode moves at the widths the kernels store (fixed iterations).
 
-    per-pass ("passes"): stage (read N·w_in, write N·ws); check pass 0 (IB: gathers the staged channel per
-    edge and writes E; float: send reads N and writes E); i_max−1 loop iterations of variable pass (read
-    E+N, write E) + check pass (read E, write E); decision (read E+N, write N·w_out) — messages at ws bytes.
+    per-pass IB (ws < 4): stage (read N·w_in, write N·ws); check pass 0 (gathers the staged channel per edge,
+    writes E); i_max−1 loop iterations of variable pass (read E+N, write E) + check pass (read E, write E);
+    decision (read E+N, write N·w_out) — messages at ws bytes.
+    per-pass float (ws >= 4): stage; send (read N, write E); i_max−1 check passes (read E, write E; the
+    i_max−2 that fold `folded` degree-2 variables also read their 2 channel rows); i_max−2 variable passes
+    (the last iteration's feeds no output and is not run) over the unfolded variables (read E'+N', write E',
+    E' = E − 2·folded, N' = N − folded); decision.
     fused ("fused"): channel in (N·w_in), the transposed staging copy (N·w_stage written and read: u8 for IB,
     the float width for min-sum / BP), output out (N·w_out); the messages never leave LDS."""
     E, N = n_e, n_v
     if path == "fused":
         return N * w_in + 2 * N * w_stage + N * w_out
-    return (N * w_in + N * ws + (E + N if ws >= 4 else 2 * E) * ws
-            + (imax - 1) * (4 * E + N) * ws + (E + N) * ws + N * w_out)
+    if ws < 4:
+        return (N * w_in + N * ws + 2 * E * ws
+                + (imax - 1) * (4 * E + N) * ws + (E + N) * ws + N * w_out)
+    nf = folded
+    loop = 0
+    if imax >= 2:
+        loop = (imax - 1) * 2 * E + (imax - 2) * (2 * nf + 2 * (E - 2 * nf) + (N - nf))
+    return N * w_in + N * ws + (E + N) * ws + loop * ws + (E + N) * ws + N * w_out
 
 
 LDS_CLK_GHZ = 2.4          # MI355X max engine clock (MI355X_MICROARCH.md chip table)
@@ -126,7 +147,7 @@ def _pmc_traffic(path, kind, kname, B, fmt):
     return None
 
 
-def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec):
+def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec, folded=0):
     """Roofline of the dominant kernel, priced at the bytes it actually moves.
 
     Per-pass kernels (HBM-bound by design): check pass reads E message rows and writes E; variable
@@ -137,6 +158,12 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
     79 B/clk/CU, MI355X_MICROARCH.md §LDS), with its HBM bytes (channel in, APP out) reported beside."""
     cn_bytes_u8 = 2 * g.n_e * w * B
     vn_bytes_u8 = (2 * g.n_e * w + n_v * w) * B
+    if folded and fmt == "f32":
+        # degree-2 fold (float per-pass): the variable pass covers E - 2 nf edges and N - nf variables; the
+        # check passes that fold (all but the last of cn_n) also read 2 channel rows per folded variable
+        vn_bytes_u8 = (2 * (g.n_e - 2 * folded) + (n_v - folded)) * w * B
+        fold_frac = max(cn_n - 1, 0) / max(cn_n, 1)
+        cn_bytes_u8 = int(round((2 * g.n_e + 2 * folded * fold_frac) * w * B))
 
     def cn_lk(d):     # table lookups of one check of degree d per codeword (prefix sharing, matching composed)
         return (2 if match else 0) if d == 2 else (d - 2) + d * (d - 1) // 2 - 1
@@ -211,6 +238,14 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
             if fmt == "u4" else None,
             "launches": {"cn": cn_n, "vn": vn_n},
             "avg_ms": {"cn": round(cn_avg, 4), "vn": round(vn_avg, 4)}}
+    if fmt == "f32":
+        # both passes of the per-pass float path against HBM (bytes per launch at fp32)
+        roof["passes"] = {k: {"bytes_per_launch": int(b * ws / w), "avg_launch_ms": round(t_, 4),
+                              "achieved": round(b * ws / w / (t_ * 1e-3) / 1e9, 1) if t_ > 0 else 0.0,
+                              "frac": round(b * ws / w / (t_ * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if t_ > 0 else 0.0}
+                          for k, b, t_ in (("cn", cn_bytes_u8, cn_avg), ("vn", vn_bytes_u8, vn_avg))}
+        if folded:
+            roof["folded_degree2_variables"] = folded
     if fmt == "u4":
         # table lookups per codeword and pass of the fast path, per CU and clock at the max clock; the LDS
         # serves at most 32 conflict-free ds_read_u8 lanes/clk/CU
@@ -450,27 +485,41 @@ def main():
     g = graph.build_graph(H)
     G = engine.Graph(g, dev)
     q = UniformQuantizer(sigma2_from_ebn0(a.ebn0, g.R_c), 16)
-    gen = torch.Generator(device=dev)
-    start, _ = distributed.shard_range(B * world, rank, world)
-    gen.manual_seed(1_000_003 + start)
+    # channel of global batch gb = batch_offset + rank: the device Philox stream (ibl_channel_sample) under key
+    # CH_SEED at counter gb * philox_blocks(N, B) — the frames a 1-GPU run with --batch-offset gb decodes, so a
+    # k-GPU line's decoded_bit_errors equals the sum of the 1-GPU lines over the same global batches
+    gbatch = a.batch_offset + rank
+    ch_offset = gbatch * engine.philox_blocks(n_v, B)
     L = __import__("informationbottleneckdecodingldpc_amd._lib", fromlist=["x"]).load()
+    early = bool(a.early_stop)
+    its = torch.zeros(max(a.steps, 1), dtype=torch.int32, device=dev)   # stop iteration of every timed step
+    step_k = [0]
+
+    def it_slot():
+        return its[min(step_k[0], its.numel() - 1):][:1]
 
     if a.kind == "ib":
-        tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+        if early:
+            # LLR-derived tables (an approximate BP in the T=16 alphabet) so the batch can converge and stop
+            tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, I)
+            match = True
+        else:
+            tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
         dec = engine.IBDecoder(G, tb, match, B, path=a.path)
-        ch = q.sample_all_zero_device(n_v, B, dev, generator=gen)
+        ch = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
+        engine.channel_sample(ch, q.cdf_t_given_x_equals_zero, CH_SEED, ch_offset)
         out = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
-        run = lambda: dec.decode(ch, out=out, early_stop=False)     # noqa: E731
+        run = lambda: dec.decode(ch, out=out, early_stop=early, iters=it_slot())     # noqa: E731
         timing_on = lambda on: L.ibl_ib_timing(dec._h, int(on))    # noqa: E731
         timing_read_fn = L.ibl_ib_timing_read
         w, dtype = 1, "u8"
     else:
         kind = 0 if a.kind == "minsum" else 1
         dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.path)
-        cl = q.sample_all_zero_device(n_v, B, dev, generator=gen, dtype=torch.int64)
-        llr = torch.as_tensor(q.output_LLRs, dtype=torch.float32, device=dev)[cl].contiguous()
+        llr = torch.empty((n_v, B), dtype=torch.float32, device=dev)
+        engine.channel_sample(llr, q.cdf_t_given_x_equals_zero, CH_SEED, ch_offset, llr=q.output_LLRs)
         out = torch.empty((n_v, B), dtype=torch.float32, device=dev)
-        run = lambda: dec.decode(llr, out=out, early_stop=False)    # noqa: E731
+        run = lambda: dec.decode(llr, out=out, early_stop=early, iters=it_slot())    # noqa: E731
         timing_on = lambda on: L.ibl_float_timing(dec._h, int(on))  # noqa: E731
         timing_read_fn = L.ibl_float_timing_read
         w, dtype = 4, "f32"
@@ -491,7 +540,8 @@ def main():
     torch.cuda.synchronize(dev)
     timing_on(True)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for k in range(a.steps):
+        step_k[0] = k
         run()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -510,6 +560,8 @@ def main():
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
     fused = dec.fused
+    folded = 0 if (a.kind == "ib" or fused) else dec.folded
+    stop_it = its[:a.steps].cpu().numpy() if a.steps > 0 else np.zeros(1, np.int32)
     fast = a.kind == "ib" and getattr(dec, "fast_path", False)
     # bytes per stored message / channel value as this build moves them: the IB fast path keeps 4-bit
     # nibbles (2 codewords per byte), the generic IB path u8, the float paths fp32
@@ -517,12 +569,13 @@ def main():
     fmt = "u4" if fast else ("u8" if a.kind == "ib" else "f32")
     if a.kind == "ib":
         dtype = fmt
-    roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec)
+    roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec,
+                    folded=folded)
     # HBM bytes the decode moves per codeword at the stored widths (channel in, output out: u8 for IB, fp32 float)
-    moved = moved_bytes_per_cw(g.n_e, n_v, I, "fused" if fused else "passes", ws, w, w, w_stage=w)
+    moved = moved_bytes_per_cw(g.n_e, n_v, I, "fused" if fused else "passes", ws, w, w, w_stage=w, folded=folded)
     cpu = None
     code_name, code_desc = CODES[a.code]
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not early:   # the baseline times fixed iterations
         cpu = cpu_baseline(a, g, arrays, I, B, match, ch if a.kind == "ib" else llr, out, code_name)
 
     if rank == 0:
@@ -540,15 +593,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": dtype,
-            "data": f"synthetic: all-zero codeword, BPSK/AWGN at Eb/N0 {a.ebn0} dB quantised to 16 clusters; "
-                    f"{'random T=16 IB tables' if a.kind == 'ib' else 'cluster LLRs'}; {code_desc}",
+            "data": f"synthetic: all-zero codeword, BPSK/AWGN at Eb/N0 {a.ebn0} dB quantised to 16 clusters "
+                    f"(device Philox, key {CH_SEED}, global batch {a.batch_offset}+rank); "
+                    f"{('LLR-derived T=16 IB tables' if early else 'random T=16 IB tables') if a.kind == 'ib' else 'cluster LLRs'}"
+                    f"; {code_desc}",
             "config": {"workload": f"{code_name}, "
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, "
                                    f"{('matching ' + ('on' if match else 'off') + ', ') if a.kind == 'ib' else ''}"
                                    f"{'fused on-chip kernel' if fused else 'per-pass kernels'}"
-                                   f", fixed iterations",
+                                   f"{', early stop on (batch-global)' if early else ', fixed iterations'}",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
+                       "early_stop": early, "ebn0_db": a.ebn0, "batch_offset": a.batch_offset,
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
             "hbm_gbps_algorithmic": round(value * moved / 1e9, 1),
             "bytes_per_codeword": int(round(moved)),
@@ -563,6 +619,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "decoded_bit_errors": tot["errors"], "decoded_bits": tot["bits"],
+            # stop iteration L the decoder reports (ibl_*_decode d_iters; i_max - 1 = ran every iteration), rank 0
+            "stop_iteration": {"min": int(stop_it.min()), "max": int(stop_it.max()), "imax": I},
+            "latency_ms_per_decode": round(elapsed / max(a.steps, 1) * 1e3, 4),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -163,6 +163,22 @@ void ibl_float_destroy(ibl_float* h);
  */
 int ibl_float_set_path(ibl_float* h, int32_t path);
 int ibl_float_path_in_use(const ibl_float* h, int32_t* fused);
+/*
+ * Degree-2 variable fold of the per-pass path (no reference counterpart; outputs are identical with and
+ * without it): the check pass that produces a degree-2 variable's input also computes that variable's
+ * output message (clamp(ch + m), kernels_min_and_BP.cl:110-118) into the next check pass's inbox, and the
+ * variable pass skips the variable.  *n_folded = number of folded variables (0: off — no degree-2
+ * variables, or IBL_FL_FOLD=0 in the environment when the decoder was created).
+ */
+int ibl_float_folded(const ibl_float* h, int32_t* n_folded);
+/*
+ * Channel-LLR precondition check (no reference counterpart).  The staging step of every ibl_float_decode
+ * counts the channel LLRs that break ibl_float_decode's precondition — NaN (min-sum); NaN, +-inf or
+ * |x| > 354 (BP) — on the device, without a host sync.  This call synchronises `stream`, stores that count
+ * since the previous call in *violations (may be NULL), clears it, and returns IBL_EINVAL (message in
+ * ibl_last_error) when it is not 0: the outputs of those decodes are unspecified.
+ */
+int ibl_float_input_check(ibl_float* h, int32_t* violations, void* stream);
 int ibl_float_timing(ibl_float* h, int32_t enable);
 int ibl_float_timing_read(ibl_float* h, double* cn_ms, int32_t* cn_launches, double* vn_ms, int32_t* vn_launches);
 

@@ -79,6 +79,7 @@ struct ibl_graph {
   int64_t n_e = 0;
   int32_t dcm = 0, dvm = 0;
   std::vector<int32_t> h_cn_deg, h_vn_deg;
+  std::vector<int32_t> h_cn_start, h_cols, h_vn_start, h_tgt_vn;   // host copies (fold / fused task set-up)
   int32_t *cn_start = nullptr, *cn_deg = nullptr, *tgt_cn = nullptr;
   int32_t *vn_start = nullptr, *vn_deg = nullptr, *tgt_vn = nullptr, *csr_cols = nullptr;
   // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable)
@@ -193,6 +194,12 @@ struct ibl_float {
   void *cin = nullptr, *vbuf0 = nullptr, *vbuf1 = nullptr, *chf = nullptr;
   int32_t *flags = nullptr, *dL = nullptr;
   int grid_cn = 0, grid_vn = 0;
+  // degree-2 variable fold of the per-pass path (fl_cn_item): per-check records, the variables the
+  // variable pass still updates, the second check inbox (the check passes alternate between cin / cin2)
+  void* cin2 = nullptr;
+  int32_t *fold = nullptr, *vn_nodes = nullptr;
+  int32_t n_vn_nodes = 0, n_folded = 0;
+  int32_t* bad = nullptr;   // channel LLRs that violated the precondition since the last ibl_float_input_check
   KTimer timer;
   // fused on-chip path (FlFusedArgs): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
@@ -277,6 +284,10 @@ int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int3
   g->dvm = *std::max_element(vd.begin(), vd.end());
   g->h_cn_deg = cd;
   g->h_vn_deg = vd;
+  g->h_cn_start = cs;
+  g->h_cols.assign(cols, cols + E);
+  g->h_vn_start = vs;
+  g->h_tgt_vn = tv;
   if ((rc = dupload(&g->cn_start, cs.data(), n_c)) || (rc = dupload(&g->cn_deg, cd.data(), n_c)) ||
       (rc = dupload(&g->tgt_cn, tc.data(), E)) || (rc = dupload(&g->vn_start, vs.data(), n_v)) ||
       (rc = dupload(&g->vn_deg, vd.data(), n_v)) || (rc = dupload(&g->tgt_vn, tv.data(), E)) ||
@@ -823,6 +834,44 @@ struct FusedTasks {
   std::vector<int32_t> cn_task, vn_task, vn_node, vn_slot;
 };
 int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order);
+
+// Degree-2 variable fold (FlArgs::fold, fl_cn_item): a degree-2 variable v on checks c1, c2 is folded when
+// both checks have one of their two fold slots free (variables taken in ascending order); each check's record
+// names v's edge position in the check, the check-order row of v's other edge and v. Returns the folded
+// variables' count; `rec` gets n_c records, `rest` the variables the variable pass still updates.
+int32_t plan_fold(const ibl_graph* g, std::vector<int32_t>* rec, std::vector<int32_t>* rest) {
+  const int32_t nc = g->n_c, nv = g->n_v;
+  rec->assign((size_t)nc * kFoldRec, 0);
+  std::vector<int32_t> used(nc, 0);
+  for (int32_t c = 0; c < nc; ++c) (*rec)[(size_t)kFoldRec * c] = (*rec)[(size_t)kFoldRec * c + 1] = -1;
+  // check of each check-order edge
+  std::vector<int32_t> chk_of(g->h_cols.size());
+  for (int32_t c = 0; c < nc; ++c)
+    for (int32_t k = 0; k < g->h_cn_deg[c]; ++k) chk_of[(size_t)g->h_cn_start[c] + k] = c;
+  std::vector<char> folded(nv, 0);
+  int32_t n = 0;
+  for (int32_t v = 0; v < nv; ++v) {
+    if (g->h_vn_deg[v] != 2) continue;
+    const int32_t e1 = g->h_tgt_vn[(size_t)g->h_vn_start[v]], e2 = g->h_tgt_vn[(size_t)g->h_vn_start[v] + 1];
+    const int32_t c1 = chk_of[(size_t)e1], c2 = chk_of[(size_t)e2];
+    if (used[c1] >= 2 || used[c2] >= 2) continue;
+    auto put = [&](int32_t c, int32_t e, int32_t other) {
+      int32_t* r = &(*rec)[(size_t)kFoldRec * c];
+      const int k = used[c]++;
+      r[k] = e - g->h_cn_start[c];
+      r[2 + k] = other;
+      r[4 + k] = v;
+    };
+    put(c1, e1, e2);
+    put(c2, e2, e1);
+    folded[v] = 1;
+    ++n;
+  }
+  rest->clear();
+  for (int32_t v = 0; v < nv; ++v)
+    if (!folded[v]) rest->push_back(v);
+  return n;
+}
 int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_task, int32_t** vn_node, int32_t** vn_slot) {
   int rc;
   if ((rc = dupload(cn_task, ft.cn_task.data(), ft.cn_task.size())) || (rc = dupload(vn_task, ft.vn_task.data(), ft.vn_task.size())) ||
@@ -1046,6 +1095,29 @@ int ibl_float_set_path(ibl_float* h, int32_t path) {
   return IBL_OK;
 }
 
+int ibl_float_folded(const ibl_float* h, int32_t* n_folded) {
+  if (!h || !n_folded) return fail(IBL_EINVAL, "NULL argument");
+  *n_folded = h->n_folded;
+  return IBL_OK;
+}
+
+int ibl_float_input_check(ibl_float* h, int32_t* violations, void* stream) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(h->g->device));
+  int32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, h->bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemsetAsync(h->bad, 0, sizeof(int32_t), s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (violations) *violations = n;
+  if (n > 0)
+    return fail(IBL_EINVAL, std::to_string(n) + (h->kind == IBL_BP
+                                                     ? " channel LLR(s) NaN, infinite or |x| > 354 (BP precondition)"
+                                                     : " channel LLR(s) NaN (min-sum precondition)") +
+                                ": those decodes' outputs are unspecified");
+  return IBL_OK;
+}
+
 int ibl_float_path_in_use(const ibl_float* h, int32_t* fused) {
   if (!h || !fused) return fail(IBL_EINVAL, "NULL argument");
   *fused = (h->fused_ok && h->path != IBL_PATH_PASSES) ? 1 : 0;
@@ -1072,12 +1144,13 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   uint8_t *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
   if ((rc = dalloc(&a, inbox)) || (rc = dalloc(&b, inbox)) || (rc = dalloc(&c, inbox)) ||
       (rc = dalloc(&d, (size_t)g->n_v * h->ldb * es)) || (rc = dalloc(&h->flags, (size_t)imax * kShards)) ||
-      (rc = dalloc(&h->dL, 1))) {
+      (rc = dalloc(&h->dL, 1)) || (rc = dalloc(&h->bad, 1))) {
     dfree(a); dfree(b); dfree(c); dfree(d);
     return bail(rc);
   }
   h->cin = a; h->vbuf0 = b; h->vbuf1 = c; h->chf = d;
-  if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess)
+  if (hipMemset(a, 0, inbox) != hipSuccess || hipMemset(b, 0, inbox) != hipSuccess || hipMemset(c, 0, inbox) != hipSuccess ||
+      hipMemset(h->bad, 0, sizeof(int32_t)) != hipSuccess)
     return bail(fail(IBL_EHIP, "hipMemset failed"));
   int bpc = 0;
   // at most 16 waves per CU: with a second block per CU its waves issue behind the first block's
@@ -1087,6 +1160,21 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_vn = std::min(bpc, 1024 / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
   if ((rc = fused_setup(h))) return bail(rc);
+  {  // degree-2 variable fold of the per-pass path (IBL_FL_FOLD=0 at create turns it off: A/B)
+    const char* fe = getenv("IBL_FL_FOLD");
+    std::vector<int32_t> rec, rest;
+    if (!(fe && fe[0] == '0') && (h->n_folded = plan_fold(g, &rec, &rest)) > 0) {
+      h->n_vn_nodes = (int32_t)rest.size();
+      uint8_t* c2 = nullptr;
+      rc = dalloc(&c2, inbox);
+      h->cin2 = c2;
+      if (rc || (rc = dupload(&h->fold, rec.data(), rec.size())) || (rc = dupload(&h->vn_nodes, rest.data(), rest.size())))
+        return bail(rc);
+      if (hipMemset(h->cin2, 0, inbox) != hipSuccess) return bail(fail(IBL_EHIP, "hipMemset failed"));
+    } else {
+      h->n_folded = 0;
+    }
+  }
   {  // same guard as the IB fast path: the float kernels are built to run without scratch
     size_t priv = 0;
     const char* kname = "";
@@ -1103,6 +1191,7 @@ void ibl_float_destroy(ibl_float* h) {
   if (!h) return;
   (void)hipSetDevice(h->g->device);
   dfree(h->cin); dfree(h->vbuf0); dfree(h->vbuf1); dfree(h->chf); dfree(h->flags); dfree(h->dL);
+  dfree(h->cin2); dfree(h->fold); dfree(h->vn_nodes); dfree(h->bad);
   dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
   delete h;
 }
@@ -1121,9 +1210,10 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   const bool early = early_stop != 0 && I > 1;
   const int cwl = h->prec == kF32 ? 4 : 2;
   const int nchunks = (B + 64 * cwl - 1) / (64 * cwl);
+  const int rule = h->kind == IBL_BP ? 2 : 1;   // the staging kernels count precondition violations
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
   if (h->fused_ok && h->path != IBL_PATH_PASSES) {
-    HIPCHK(launch_fl_stage_t(d_llr, llr_dtype, g->n_v, B, h->f_vn_node, h->chf, h->prec, s));
+    HIPCHK(launch_fl_stage_t(d_llr, llr_dtype, g->n_v, B, h->f_vn_node, h->chf, h->prec, rule, h->bad, s));
     FlFusedArgs fa{};
     fa.ch = h->chf; fa.cn_task = h->f_cn_task; fa.vn_task = h->f_vn_task; fa.vn_node = h->f_vn_node;
     fa.vn_slot = h->f_vn_slot; fa.out = d_out; fa.unsat = early ? h->flags : nullptr; fa.dL = nullptr;
@@ -1163,26 +1253,41 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     }
     return IBL_OK;
   }
-  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, s));
+  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, rule, h->bad, s));
   FlArgs send{};
-  send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
+  send.ch = h->chf; send.out = h->cin;   // = cb[1] below send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
   send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;
   HIPCHK(launch_fl_send(send, h->prec, s));
+  // Check pass j reads check inbox cb[j & 1] (send fills cb[1]) and writes the variable inbox vbuf[j & 1];
+  // variable pass j writes cb[(j + 1) & 1]. With the fold, check pass j also writes its folded variables'
+  // messages into cb[(j + 1) & 1], and the variable pass skips them; the last check pass writes every
+  // variable-inbox row (the decision reads them) and folds nothing. The last iteration's variable pass
+  // only feeds a syndrome the reference never reads (its loop ends at imax, bp_decoder_irreg.py:240-268),
+  // so it is not run.
+  const bool fold = h->n_folded > 0;
+  void* cb[2] = {fold ? h->cin2 : h->cin, h->cin};
   FlArgs cn{}, vn{};
-  cn.in = h->cin; cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn;
-  vn.out = h->cin; vn.ch = h->chf; vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn;
+  cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.ch = h->chf; cn.fold = h->fold;
+  vn.ch = h->chf; vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn;
+  vn.nodes = fold ? h->vn_nodes : nullptr;
   cn.llr_max = vn.llr_max = h->llr_max;
-  cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+  cn.n_nodes = g->n_c; vn.n_nodes = fold ? h->n_vn_nodes : g->n_v;
   cn.nchunks = vn.nchunks = nchunks;
   cn.ldb = vn.ldb = h->ldb;
   cn.B = vn.B = B;
   for (int j = 1; j < I; ++j) {
     void* vb = (j & 1) ? h->vbuf1 : h->vbuf0;
+    const bool last = j == I - 1;
+    cn.in = cb[j & 1];
     cn.out = vb;
+    cn.fout = cb[(j + 1) & 1];
+    cn.fold_mode = (fold && !last) ? (early ? 2 : 1) : 0;
     cn.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
     cn.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
     HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn(cn, h->kind, h->prec, h->g->dcm, h->grid_cn, s); }));
+    if (last) break;
     vn.in = vb;
+    vn.out = cb[(j + 1) & 1];
     vn.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
     HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn(vn, h->prec, h->g->dvm, h->grid_vn, s); }));
   }

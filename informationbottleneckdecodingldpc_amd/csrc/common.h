@@ -177,7 +177,16 @@ struct FlArgs {
   int32_t* unsat;
   double llr_max;
   int32_t n_nodes, nchunks, ldb, B;
+  // degree-2 variable fold (check pass; see fl_cn_item): per check kFoldRec ints {pos0, pos1, dst0, dst1,
+  // var0, var1, 0, 0} — edge position of up to two folded variables (-1: none), the check-order row of the
+  // variable's other edge in fout, the variable (channel row). fold_mode 0: off; 1: a folded edge's output
+  // goes to fout only; 2: to fout and to the variable inbox (early stop: any pass may be the last).
+  const int32_t* fold;
+  void* fout;               // the next check pass's inbox (check order)
+  int32_t fold_mode;
+  const int32_t* nodes;     // variable pass: node list (the variables not folded), nullptr = 0..n_nodes-1
 };
+constexpr int kFoldRec = 8;
 
 // Fused float decoder: a workgroup keeps Vec<F>::N codewords (one 16-byte slot per edge) entirely
 // in LDS for all iterations. Edge slots are numbered per check-node task (up to 64 check nodes of
@@ -267,9 +276,11 @@ hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int
                               unsigned long long* cnt, hipStream_t s);
 
 hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s);
-hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s);
+// rule: channel-LLR precondition counted into *bad (0 none, 1 NaN, 2 NaN / inf / |x| > 354; float_kernels.hip llr_bad)
+hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, int rule,
+                           int32_t* bad, hipStream_t s);
 hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm, void* dst, int prec,
-                             hipStream_t s);
+                             int rule, int32_t* bad, hipStream_t s);
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);

@@ -126,12 +126,16 @@ __device__ __forceinline__ bool fl_gate(const int32_t* gate, int lane) {
 // variable nodes: 136 -> 85 VGPRs, +14 %); degrees <= 8 keep their outputs and store them together
 // at the end of the item, which measured 9 % faster on DVB-S2 (3.21 -> 2.93 ms per VN pass).
 template <typename F>
-__device__ __forceinline__ void fl_store(const FlArgs& a, int row, int cw0, const F (&v)[Vec<F>::N]) {
+__device__ __forceinline__ void fl_store_to(void* base, int ldb, int row, int cw0, const F (&v)[Vec<F>::N]) {
   using V = Vec<F>;
   typename V::T o;
 #pragma unroll
   for (int s = 0; s < V::N; ++s) V::set(o, s, v[s]);
-  *reinterpret_cast<typename V::T*>(reinterpret_cast<F*>(a.out) + (size_t)row * a.ldb + cw0) = o;
+  *reinterpret_cast<typename V::T*>(reinterpret_cast<F*>(base) + (size_t)row * ldb + cw0) = o;
+}
+template <typename F>
+__device__ __forceinline__ void fl_store(const FlArgs& a, int row, int cw0, const F (&v)[Vec<F>::N]) {
+  fl_store_to<F>(a.out, a.ldb, row, cw0, v);
 }
 
 template <typename F, int D>
@@ -139,18 +143,21 @@ struct FlOut {
   static constexpr bool kImmediate = D > 8;
   static constexpr int N = Vec<F>::N;
   F v[kImmediate ? 1 : D][N];
-  __device__ __forceinline__ void put(const FlArgs& a, const int (&tg)[D], int cw0, int w, const F (&o)[N]) {
+  // sink(w, o) stores output w
+  template <class Sink>
+  __device__ __forceinline__ void put(int w, const F (&o)[N], Sink&& sink) {
     if constexpr (kImmediate) {
-      fl_store<F>(a, tg[w], cw0, o);
+      sink(w, o);
     } else {
 #pragma unroll
       for (int s = 0; s < N; ++s) v[w][s] = o[s];
     }
   }
-  __device__ __forceinline__ void flush(const FlArgs& a, const int (&tg)[D], int cw0) {
+  template <class Sink>
+  __device__ __forceinline__ void flush(Sink&& sink) {
     if constexpr (!kImmediate) {
 #pragma unroll
-      for (int w = 0; w < D; ++w) fl_store<F>(a, tg[w], cw0, v[w]);
+      for (int w = 0; w < D; ++w) sink(w, v[w]);
     }
   }
 };
@@ -340,8 +347,15 @@ __device__ __forceinline__ void fl_cn_body(const F (&m)[D][NC], F lm, Put&& put)
 }
 
 
+// Degree-2 variable fold (FlArgs::fold): a degree-2 variable's update is one add and a clamp per output,
+// out(c1) = clamp(ch + m(c2 -> v)) (kernels_min_and_BP.cl:110-118; fl_vn_body<D=2> in the same order), so
+// the check that produces m(c2 -> v) writes v's message to c1 itself, straight into the next check pass's
+// inbox (fout, double-buffered: this pass never reads what it writes), and the variable pass skips v. Per
+// folded variable and codeword that moves 2 channel reads instead of the variable pass's 2 message reads,
+// 1 channel read and 2 message writes; the outputs are the same bits.
 template <int KIND, typename F, int D>
-__device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, bool do_par, int valid, bool& unsat) {
+__device__ __forceinline__ void fl_cn_item(const FlArgs& a, int node, int st, int cw0, bool do_par, int valid,
+                                           bool& unsat) {
   using V = Vec<F>;
   constexpr int N = V::N;
   const F* src = reinterpret_cast<const F*>(a.in);
@@ -356,13 +370,46 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int st, int cw0, boo
 #pragma unroll
     for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
   }
+  // fold record: wave-uniform (scalar) positions, rows and variables; the channel rows load with the inputs
+  int fp0 = -1, fp1 = -1, fd0 = 0, fd1 = 0;
+  F c0[N], c1[N];
+  if (a.fold_mode) {
+    const int* fr = a.fold + (size_t)kFoldRec * node;
+    fp0 = sload(fr, 0);
+    fp1 = sload(fr, 1);
+    fd0 = sload(fr, 2);
+    fd1 = sload(fr, 3);
+    const F* ch = reinterpret_cast<const F*>(a.ch);
+    if (fp0 >= 0) {
+      const typename V::T r = *reinterpret_cast<const typename V::T*>(ch + (size_t)sload(fr, 4) * a.ldb + cw0);
+#pragma unroll
+      for (int s = 0; s < N; ++s) c0[s] = V::get(r, s);
+    }
+    if (fp1 >= 0) {
+      const typename V::T r = *reinterpret_cast<const typename V::T*>(ch + (size_t)sload(fr, 5) * a.ldb + cw0);
+#pragma unroll
+      for (int s = 0; s < N; ++s) c1[s] = V::get(r, s);
+    }
+  }
   if (do_par) {
 #pragma unroll
     for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
   }
+  auto fold_put = [&](int w, const F (&c)[N], int row, const F (&o)[N]) __attribute__((always_inline)) {
+    F f[N];
+#pragma unroll
+    for (int s = 0; s < N; ++s) f[s] = clampllr(c[s] + o[s], lm);
+    fl_store_to<F>(a.fout, a.ldb, row, cw0, f);
+    if (a.fold_mode == 2) fl_store<F>(a, tg[w], cw0, o);
+  };
+  auto sink = [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+    if (w == fp0) fold_put(w, c0, fd0, o);
+    else if (w == fp1) fold_put(w, c1, fd1, o);
+    else fl_store<F>(a, tg[w], cw0, o);
+  };
   FlOut<F, D> ob;
-  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(a, tg, cw0, w, o); });
-  ob.flush(a, tg, cw0);
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(w, o, sink); });
+  ob.flush(sink);
 }
 
 // Variable-node body on channel c and inputs m; put(w, o) receives extrinsic output w.
@@ -430,9 +477,10 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 #pragma unroll
     for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
   }
+  auto sink = [&](int w, const F (&o)[N]) __attribute__((always_inline)) { fl_store<F>(a, tg[w], cw0, o); };
   FlOut<F, D> ob;
-  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(a, tg, cw0, w, o); });
-  ob.flush(a, tg, cw0);
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(w, o, sink); });
+  ob.flush(sink);
 }
 
 #define FL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
@@ -486,7 +534,7 @@ __global__ __launch_bounds__((fl_block_of<0, MAXD, KIND, F>())) void fl_cn(FlArg
     const int cw0 = chunk * CH + lane * CWL;
     const int valid = a.B - cw0;
     switch (d) {
-#define X(D) case D: if constexpr (D <= MAXD) fl_cn_item<KIND, F, D>(a, st, cw0, do_par, valid, unsat); break;
+#define X(D) case D: if constexpr (D <= MAXD) fl_cn_item<KIND, F, D>(a, node, st, cw0, do_par, valid, unsat); break;
       FL_DEG_CASES(X)
 #undef X
       default: break;
@@ -509,8 +557,9 @@ __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
   for (;;) {
     const int item = fl_next_item(&ctr, lane, wpb, nw);
     if (item >= nitems) break;
-    const int node = __builtin_amdgcn_readfirstlane(item / a.nchunks);
-    const int chunk = __builtin_amdgcn_readfirstlane(item - node * a.nchunks);
+    const int pos = __builtin_amdgcn_readfirstlane(item / a.nchunks);
+    const int chunk = __builtin_amdgcn_readfirstlane(item - pos * a.nchunks);
+    const int node = a.nodes ? sload(a.nodes, pos) : pos;   // the fold's variable list skips folded nodes
     const int d = sload(a.deg, node), st = sload(a.start, node);
     const int cw0 = chunk * CH + lane * CWL;
     switch (d) {
@@ -578,19 +627,53 @@ __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
   }
 }
 
-// channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded, -0 stored as +0
+// Channel-LLR precondition (ibldpc.h, ibl_float_input_check): rule 1 (min-sum) flags NaN, rule 2 (BP) NaN, +-inf
+// and |x| > 354; rule 0 checks nothing. On the bit pattern of the caller's value: this source is built with
+// -fno-honor-nans, under which a float compare may be folded as if NaN did not exist.
+__device__ __forceinline__ bool llr_bad(float x, int rule) {
+  const uint32_t u = __float_as_uint(x) & 0x7fffffffu;
+  return rule != 0 && u > (rule == 2 ? 0x43b10000u : 0x7f800000u);
+}
+__device__ __forceinline__ bool llr_bad(double x, int rule) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x) & 0x7fffffffffffffffull;
+  return rule != 0 && u > (rule == 2 ? 0x4076200000000000ull : 0x7ff0000000000000ull);
+}
+// one count per wave that saw violations (rare path: the check itself is one compare per value)
+__device__ __forceinline__ void llr_count(int32_t* bad, bool b) {
+  const uint64_t m = __ballot(b);
+  if (m && (fl_tid() & 63) == __builtin_amdgcn_readfirstlane(__builtin_ctzll(m)))
+    atomicAdd(bad, (int)__builtin_popcountll(m));
+}
+
+// channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded, -0 stored as +0; counts inputs that
+// violate the precondition of `rule` into *bad
 template <typename F>
-__global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb) {
+__global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb, int rule, int32_t* bad) {
   const size_t total = (size_t)n * ldb;
-  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < total; i += (size_t)fl_gdim() * fl_bdim()) {
-    const int row = (int)(i / ldb);
-    const int b = (int)(i - (size_t)row * ldb);
-    F v = F(0);
-    if (b < B) {
-      const size_t k = (size_t)row * B + b;
-      v = in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k] : (F)reinterpret_cast<const double*>(x)[k];
+  const size_t stride = (size_t)fl_gdim() * fl_bdim();
+  // whole waves iterate together (the ballot in llr_count): the loop bound is rounded up to the stride
+  const size_t span = (total + stride - 1) / stride * stride;
+  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < span; i += stride) {
+    bool b_ = false;
+    if (i < total) {
+      const int row = (int)(i / ldb);
+      const int b = (int)(i - (size_t)row * ldb);
+      F v = F(0);
+      if (b < B) {
+        const size_t k = (size_t)row * B + b;
+        if (in_dtype == kF32) {
+          const float xv = reinterpret_cast<const float*>(x)[k];
+          b_ = llr_bad(xv, rule);
+          v = (F)xv;
+        } else {
+          const double xv = reinterpret_cast<const double*>(x)[k];
+          b_ = llr_bad(xv, rule);
+          v = (F)xv;
+        }
+      }
+      dst[i] = v + F(0);   // -0 -> +0 (equal values; see sign_xor)
     }
-    dst[i] = v + F(0);   // -0 -> +0 (equal values; see sign_xor)
+    if (rule) llr_count(bad, b_);
   }
 }
 
@@ -603,7 +686,7 @@ __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int 
 // load element by element.
 template <typename F>
 __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm,
-                                                  typename Vec<F>::T* dst) {
+                                                  typename Vec<F>::T* dst, int rule, int32_t* bad) {
   using V = Vec<F>;
   using VT = typename V::T;
   constexpr int N = V::N, P = 64, G = 32, RW = G + 1;
@@ -617,6 +700,7 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
     __syncthreads();
     constexpr int kPer = P * G / 256;   // cells per thread, all loads issued before the LDS stores
     VT v[kPer];
+    bool b_ = false;
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
@@ -628,15 +712,26 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
         const size_t k = (size_t)perm[p] * B + (size_t)g * N;
         if (vec) {
           v[it] = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(x) + k);
+#pragma unroll
+          for (int s = 0; s < N; ++s) b_ |= llr_bad(V::get(v[it], s), rule);
         } else {
 #pragma unroll
           for (int s = 0; s < N; ++s)
-            if (g * N + s < B)
-              V::set(v[it], s, in_dtype == kF32 ? (F)reinterpret_cast<const float*>(x)[k + s]
-                                                : (F)reinterpret_cast<const double*>(x)[k + s]);
+            if (g * N + s < B) {
+              if (in_dtype == kF32) {
+                const float xv = reinterpret_cast<const float*>(x)[k + s];
+                b_ |= llr_bad(xv, rule);
+                V::set(v[it], s, (F)xv);
+              } else {
+                const double xv = reinterpret_cast<const double*>(x)[k + s];
+                b_ |= llr_bad(xv, rule);
+                V::set(v[it], s, (F)xv);
+              }
+            }
         }
       }
     }
+    if (rule) llr_count(bad, b_);
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
@@ -931,21 +1026,26 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
 }
 
 // ---------------------------------------------------------------------- launchers
-hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, hipStream_t s) {
+hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, int rule,
+                           int32_t* bad, hipStream_t s) {
   const size_t total = (size_t)n * ldb;
   const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
-  if (prec == kF32) hipLaunchKernelGGL(fl_stage<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (float*)dst, ldb);
-  else hipLaunchKernelGGL(fl_stage<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (double*)dst, ldb);
+  if (prec == kF32)
+    hipLaunchKernelGGL(fl_stage<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (float*)dst, ldb, rule, bad);
+  else
+    hipLaunchKernelGGL(fl_stage<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, (double*)dst, ldb, rule, bad);
   return hipGetLastError();
 }
 
 hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm, void* dst, int prec,
-                             hipStream_t s) {
+                             int rule, int32_t* bad, hipStream_t s) {
   const int cwl = prec == kF32 ? 4 : 2;
   const size_t tiles = (size_t)((n + 63) / 64) * (size_t)((((B + cwl - 1) / cwl) + 31) / 32);
   const int grid = (int)std::max<size_t>(1, std::min<size_t>(tiles, 8192));
-  if (prec == kF32) hipLaunchKernelGGL(fl_stage_t<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (float4*)dst);
-  else hipLaunchKernelGGL(fl_stage_t<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (double2*)dst);
+  if (prec == kF32)
+    hipLaunchKernelGGL(fl_stage_t<float>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (float4*)dst, rule, bad);
+  else
+    hipLaunchKernelGGL(fl_stage_t<double>, dim3(grid), dim3(256), 0, s, x, in_dtype, n, B, perm, (double2*)dst, rule, bad);
   return hipGetLastError();
 }
 

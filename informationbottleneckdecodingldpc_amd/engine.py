@@ -185,6 +185,23 @@ class FloatDecoder:
         _lib.check(_lib.load().ibl_float_path_in_use(self._h, ctypes.byref(f)), "ibl_float_path_in_use")
         return bool(f.value)
 
+    @property
+    def folded(self) -> int:
+        """Degree-2 variables the per-pass path folds into the check pass (``ibl_float_folded``)."""
+        f = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_float_folded(self._h, ctypes.byref(f)), "ibl_float_folded")
+        return int(f.value)
+
+    def input_violations(self, raise_on_error: bool = True) -> int:
+        """Channel LLRs of the decodes since the last call that broke the precondition (NaN; for BP also
+        +-inf and |x| > 354): synchronises the current stream (``ibl_float_input_check``). Raises
+        :class:`_lib.IBLError` when there were any, unless ``raise_on_error`` is False."""
+        v = ctypes.c_int32()
+        rc = _lib.load().ibl_float_input_check(self._h, ctypes.byref(v), _stream_ptr(self.device))
+        if raise_on_error:
+            _lib.check(rc, "ibl_float_input_check")
+        return int(v.value)
+
     def decode(self, llr: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=None,
                early_stop: bool = True, iters: Optional[torch.Tensor] = None) -> torch.Tensor:
         n = self.graph.edges.n_v

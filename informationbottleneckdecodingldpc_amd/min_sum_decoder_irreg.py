@@ -53,7 +53,12 @@ class Min_Sum_Decoder_class_irregular(CodeMixin):
         if llr.shape[1] > self._dec.max_batch:
             self.init_OpenCL_decoding(llr.shape[1], self.device)
         out = self._dec.decode(llr, early_stop=early_stop)
-        return out if return_buffer else out.cpu().numpy()
+        if return_buffer:
+            return out
+        # host output synchronises anyway: channel LLRs that break the precondition (NaN; BP: also +-inf,
+        # |x| > 354) raise instead of returning unspecified values (FloatDecoder.input_violations)
+        self._dec.input_violations()
+        return out.cpu().numpy()
 
     def decode_OpenCL_min_sum(self, received_blocks, buffer_in=False, return_buffer=False):
         """Reference :221-287."""

@@ -91,11 +91,30 @@ def test_moved_bytes_dvbs2_u4(dvb):
     assert abs(m / 1e6 - 24.35) < 0.01
     # at the round-2 headline rate this is physically possible, while the u8 figure was not
     assert 175e3 * m / 1e9 < bench.HBM_PEAK_GBPS < 175e3 * bench.bytes_per_cw(E, N, 50, 1) / 1e9
-    # float per-pass: send reads N and writes E instead of the gather
+    # float per-pass: send reads N and writes E instead of the gather; 99 check passes, 98 variable passes
+    # (the last iteration's variable pass feeds nothing and is not run)
     f = bench.moved_bytes_per_cw(E, N, 100, "passes", 4, 4, 4)
-    assert f == 4 * N + 4 * N + 4 * (E + N) + 99 * 4 * (4 * E + N) + 4 * (E + N) + 4 * N
+    assert f == 4 * N + 4 * N + 4 * (E + N) + 4 * (99 * 2 * E + 98 * (2 * E + N)) + 4 * (E + N) + 4 * N
+    # with the degree-2 fold (C5: 32,399 variables): 98 folding check passes read 2 channel rows per folded
+    # variable; the 98 variable passes cover E - 2 nf edges and N - nf variables
+    nf = 32399
+    ff = bench.moved_bytes_per_cw(E, N, 100, "passes", 4, 4, 4, folded=nf)
+    assert ff == f + 4 * 98 * (2 * nf - 4 * nf - nf)
+    assert 0.88 < ff / f < 0.92                       # ~10 % fewer bytes per codeword
     # fused: channel in, staging copy written and read, output out
     assert bench.moved_bytes_per_cw(E, N, 50, "fused", 0.5, 1, 1, w_stage=1) == 4 * N
+
+
+def test_float_roofline_with_fold(dvb):
+    """The per-pass float roofline prices both passes; with the fold the variable pass moves E - 2 nf edge
+    rows (read + write) and N - nf channel rows, and the folding check passes read 2 nf channel rows."""
+    g, B, nf = dvb, 8192, 32399
+    r = bench.roofline(_args(kind="bp"), g, g.n_v, B, 100, 4, 4, "f32", False, False,
+                       cn_avg=3.2, vn_avg=2.2, cn_ms=3.2 * 99, vn_ms=2.2 * 98, cn_n=99, vn_n=98, dec=None, folded=nf)
+    assert r["passes"]["vn"]["bytes_per_launch"] == (2 * (g.n_e - 2 * nf) + g.n_v - nf) * 4 * B
+    assert r["passes"]["cn"]["bytes_per_launch"] == round((2 * g.n_e + 2 * nf * 98 / 99) * 4 * B)
+    assert r["kernel"] == "fl_cn" and r["folded_degree2_variables"] == nf
+    assert 0 < r["passes"]["cn"]["frac"] <= 1 and 0 < r["passes"]["vn"]["frac"] <= 1
 
 
 def test_committed_bench_lines_are_physical():

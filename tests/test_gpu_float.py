@@ -424,3 +424,103 @@ def test_float32_minsum_c3_converged_codewords_h5(eng, ebn0):
     bad = _h5(out[:, conv], ref[:, conv])
     assert bad.sum() == 0, f"{bad.sum()} LLRs of converged codewords outside H5, max |x-y| {d.max():.3e}"
     assert ((out[:, conv] < 0) == (ref[:, conv] < 0)).all()
+
+
+# ------------------------------------------------------------------ degree-2 variable fold (per-pass path)
+@pytest.mark.parametrize("prec", [torch.float32, torch.float64])
+@pytest.mark.parametrize("kind", [oracle.MINSUM, oracle.BP])
+@pytest.mark.parametrize("name,imax,B,early,ebn0", [
+    ("dvb", 12, 300, False, 1.0),     # C5's code: 32,399 degree-2 variables, every check folds two
+    ("dvb", 30, 260, True, 2.0),      # early stop: folded passes write the variable inbox too (mode 2)
+    ("dvb", 2, 7, False, 1.0),        # one check pass: it is the last, nothing folds
+    ("wlan", 20, 257, True, 1.5)])    # dual-diagonal parity: degree-2 variables of the WLAN code
+def test_float_fold_equals_unfolded(eng, prec, kind, name, imax, B, early, ebn0, wlan_H, dvb_H, monkeypatch):
+    """The fold (the check pass computes a degree-2 variable's outgoing message, clamp(ch + m) in the
+    variable pass's order, straight into the next check pass's inbox; the variable pass skips it) gives the
+    same bits and stop iteration as the unfolded per-pass path (IBL_FL_FOLD=0), fp32 and fp64, min-sum and BP;
+    fp64 min-sum also equals the oracle."""
+    H = {"dvb": dvb_H, "wlan": wlan_H}[name]
+    g = graph.build_graph(H)
+    G = eng.Graph(g, DEV)
+    llr = _llrs(g, B, ebn0, seed=imax * 3 + B, quantised=True)
+    res = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("IBL_FL_FOLD", fold)
+        dec = eng.FloatDecoder(G, kind, imax, B, precision=prec, path="passes")
+        n2 = int((np.asarray(g.vn_deg) == 2).sum())
+        if fold == "1":
+            assert dec.folded > 0 and dec.folded <= n2
+            if name == "dvb":
+                assert dec.folded == n2 == 32399
+        else:
+            assert dec.folded == 0
+        it = torch.zeros(1, dtype=torch.int32, device=DEV)
+        out = dec.decode(torch.from_numpy(llr).to(DEV).to(prec), early_stop=early, iters=it)
+        res[fold] = (out.double().cpu().numpy(), int(it.item()))
+    assert res["1"][1] == res["0"][1]
+    np.testing.assert_array_equal(res["1"][0], res["0"][0])
+    if kind == oracle.MINSUM and prec == torch.float64:
+        ref, ref_it = oracle.float_decode(g, kind, imax, llr, early_stop=early, return_iters=True)
+        assert res["1"][1] == ref_it
+        np.testing.assert_array_equal(res["1"][0], ref)
+
+
+def test_float_fold_absent_without_degree2(eng, reg_H):
+    G = eng.Graph(graph.build_graph(reg_H), DEV)
+    assert eng.FloatDecoder(G, 0, 5, 16, path="passes").folded == 0
+
+
+# ------------------------------------------------------------------ channel-LLR precondition check
+@pytest.mark.parametrize("path", ["auto", "passes"])
+def test_float_input_check(eng, wlan_H, path):
+    """ibl_float_input_check: the staging kernels count channel LLRs that break
+    ibl_float_decode's precondition — BP: NaN, +-inf, |x| > 354; min-sum: NaN only (+-inf is a known bit) —
+    and the query returns IBL_EINVAL with the count; valid inputs count 0. The BP case with +-inf inputs is
+    the one that failed in round 4 (gpurun_out/r4c2) before the precondition was narrowed."""
+    from informationbottleneckdecodingldpc_amd._lib import IBLError
+    g = graph.build_graph(wlan_H)
+    G = eng.Graph(g, DEV)
+    B = 96
+    llr = _llrs(g, B, 1.5, seed=77)
+    rng = np.random.default_rng(78)
+    pos = rng.random(llr.shape) < 0.02
+    bad_inf = llr.copy()
+    bad_inf[pos] = np.where(rng.random(pos.sum()) < 0.8, np.inf, -np.inf)
+    big = llr.copy()
+    big[0, :5] = [354.0, -354.0, 354.5, -1e6, 353.9]      # two of these break |x| <= 354
+    nan = llr.copy()
+    nan[3, 7] = np.nan
+    for prec in (torch.float32, torch.float64):
+        bp = eng.FloatDecoder(G, oracle.BP, 10, B, precision=prec, path=path)
+        ms = eng.FloatDecoder(G, oracle.MINSUM, 10, B, precision=prec, path=path)
+        for dec in (bp, ms):
+            dec.decode(torch.from_numpy(llr).to(DEV).to(prec), early_stop=False)
+            assert dec.input_violations() == 0
+        bp.decode(torch.from_numpy(bad_inf).to(DEV).to(prec), early_stop=False)
+        with pytest.raises(IBLError, match="BP precondition"):
+            bp.input_violations()
+        bp.decode(torch.from_numpy(bad_inf).to(DEV).to(prec), early_stop=False)
+        assert bp.input_violations(raise_on_error=False) == int(pos.sum())
+        assert bp.input_violations() == 0                       # cleared by the query
+        ms.decode(torch.from_numpy(bad_inf).to(DEV).to(prec), early_stop=False)
+        assert ms.input_violations() == 0                       # +-inf allowed for min-sum
+        bp.decode(torch.from_numpy(big).to(DEV).to(torch.float64), early_stop=False)
+        assert bp.input_violations(raise_on_error=False) == 2   # the f64 caller values are checked
+        for dec in (bp, ms):
+            dec.decode(torch.from_numpy(nan).to(DEV).to(prec), early_stop=False)
+            assert dec.input_violations(raise_on_error=False) == 1
+
+
+def test_dropin_bp_raises_on_invalid_channel(wlan_H):
+    """The reference-named BP class returning host arrays raises instead of handing back unspecified APP
+    LLRs for +-inf channel values (kernels_min_and_BP.cl:5-9: the reference's box-plus gives NaN there)."""
+    from informationbottleneckdecodingldpc_amd._lib import IBLError
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    g = graph.build_graph(wlan_H)
+    llr = _llrs(g, 8, 1.5, 9)
+    bp = BeliefPropagationDecoderClassIrregular(wlan_H, 20, 16, 8)
+    bp.init_OpenCL_decoding(8)
+    bp.decode_OpenCL_belief_propagation(llr)
+    llr[5, 2] = np.inf
+    with pytest.raises(IBLError):
+        bp.decode_OpenCL_belief_propagation(llr)
