@@ -1255,7 +1255,8 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   }
   HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, rule, h->bad, s));
   FlArgs send{};
-  send.ch = h->chf; send.out = h->cin;   // = cb[1] below send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
+  send.ch = h->chf; send.out = h->cin;   // = cb[1] below
+  send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
   send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;
   HIPCHK(launch_fl_send(send, h->prec, s));
   // Check pass j reads check inbox cb[j & 1] (send fills cb[1]) and writes the variable inbox vbuf[j & 1];

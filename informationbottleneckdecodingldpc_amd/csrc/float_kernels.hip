@@ -1049,7 +1049,16 @@ hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const in
   return hipGetLastError();
 }
 
+// Host-side operand checks before a launch: a missing array would fault the device, not fail the call.
+static bool fl_args_ok(const FlArgs& a, int which) {
+  if (!a.out || !a.start || !a.deg || !a.tgt || a.ldb <= 0 || a.n_nodes < 0 || a.B <= 0 || a.B > a.ldb) return false;
+  if (which == 0) return a.in && (a.fold_mode == 0 || (a.fold && a.fout && a.ch));   // check pass
+  if (which == 1) return a.in && a.ch;                                              // variable pass
+  return a.ch != nullptr;                                                           // send
+}
+
 hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s) {
+  if (!fl_args_ok(a, 2)) return hipErrorInvalidValue;
   const size_t total = (size_t)a.n_nodes * (a.ldb / 4);
   const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
   if (prec == kF32) hipLaunchKernelGGL(fl_send<float>, dim3(grid), dim3(256), 0, s, a);
@@ -1077,12 +1086,14 @@ int fl_block(int which, int kind, int prec, int maxd) {
 }
 
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s) {
+  if (!fl_args_ok(a, 0)) return hipErrorInvalidValue;
   FlArgs args = a;
   void* p[] = {&args};
   return hipLaunchKernel(fl_kernel(0, kind, prec, maxd), dim3(grid), dim3(fl_block(0, kind, prec, maxd)), p, 0, s);
 }
 
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s) {
+  if (!fl_args_ok(a, 1)) return hipErrorInvalidValue;
   FlArgs args = a;
   void* p[] = {&args};
   return hipLaunchKernel(fl_kernel(1, 0, prec, maxd), dim3(grid), dim3(fl_block(1, 0, prec, maxd)), p, 0, s);
