@@ -81,6 +81,13 @@ for s in $STEPS; do
         IBL_ALLOW_SCRATCH=1 IBL_TRACE_FUSED=$O/ftrace_$c.bin IBLDPC_LIB=$VL/libibldpc_ftrace.so timeout -k 10 300 python $R/bench.py --config $c --no-cpu-baseline --steps 1 --warmup 0 > $O/ftrace_$c.json 2> $O/ftrace_$c.err
         chk $? ftrace_$c; echo "ftrace $c ok" >> $O/summary.txt
       done;;
+    lines)   # one run per line of $LINES: "<name> [VAR=value ...] <command ...>" (relative paths from the repo root)
+      while read -r name args; do
+        [ -z "$name" ] && continue
+        case $name in \#*) continue;; esac
+        eval "timeout -k 10 300 env $args" > $O/line_$name.json 2> $O/line_$name.err
+        rc=$?; echo "line $name rc=$rc $(jf $O/line_$name.json)" >> $O/summary.txt; chk $rc line_$name
+      done < ${LINES:-tools/lines_default.txt};;
     mrank)   # N>1 bench path rehearsed on one GPU: 2 ranks sharing cuda:0 over gloo
       IBL_SHARE_DEVICE=1 IBL_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_2rank.json 2> $O/bench_2rank.err
       rc=$?; echo "mrank rc=$rc" >> $O/summary.txt; chk $rc mrank;;
