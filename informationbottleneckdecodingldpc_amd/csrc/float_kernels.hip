@@ -638,11 +638,9 @@ __device__ __forceinline__ bool llr_bad(double x, int rule) {
   const uint64_t u = (uint64_t)__double_as_longlong(x) & 0x7fffffffffffffffull;
   return rule != 0 && u > (rule == 2 ? 0x4076200000000000ull : 0x7ff0000000000000ull);
 }
-// one count per wave that saw violations (rare path: the check itself is one compare per value)
-__device__ __forceinline__ void llr_count(int32_t* bad, bool b) {
-  const uint64_t m = __ballot(b);
-  if (m && (fl_tid() & 63) == __builtin_amdgcn_readfirstlane(__builtin_ctzll(m)))
-    atomicAdd(bad, (int)__builtin_popcountll(m));
+// violations counted per lane (rare path: the check itself is one compare per value)
+__device__ __forceinline__ void llr_count(int32_t* bad, int nb) {
+  if (nb) atomicAdd(bad, nb);
 }
 
 // channel staging: user LLRs (f32/f64, [N][B]) -> F [N][ldb], zero padded, -0 stored as +0; counts inputs that
@@ -650,31 +648,26 @@ __device__ __forceinline__ void llr_count(int32_t* bad, bool b) {
 template <typename F>
 __global__ void fl_stage(const void* x, int in_dtype, int n, int B, F* dst, int ldb, int rule, int32_t* bad) {
   const size_t total = (size_t)n * ldb;
-  const size_t stride = (size_t)fl_gdim() * fl_bdim();
-  // whole waves iterate together (the ballot in llr_count): the loop bound is rounded up to the stride
-  const size_t span = (total + stride - 1) / stride * stride;
-  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < span; i += stride) {
-    bool b_ = false;
-    if (i < total) {
-      const int row = (int)(i / ldb);
-      const int b = (int)(i - (size_t)row * ldb);
-      F v = F(0);
-      if (b < B) {
-        const size_t k = (size_t)row * B + b;
-        if (in_dtype == kF32) {
-          const float xv = reinterpret_cast<const float*>(x)[k];
-          b_ = llr_bad(xv, rule);
-          v = (F)xv;
-        } else {
-          const double xv = reinterpret_cast<const double*>(x)[k];
-          b_ = llr_bad(xv, rule);
-          v = (F)xv;
-        }
+  int nb = 0;
+  for (size_t i = (size_t)fl_bid() * fl_bdim() + fl_tid(); i < total; i += (size_t)fl_gdim() * fl_bdim()) {
+    const int row = (int)(i / ldb);
+    const int b = (int)(i - (size_t)row * ldb);
+    F v = F(0);
+    if (b < B) {
+      const size_t k = (size_t)row * B + b;
+      if (in_dtype == kF32) {
+        const float xv = reinterpret_cast<const float*>(x)[k];
+        nb += llr_bad(xv, rule);
+        v = (F)xv;
+      } else {
+        const double xv = reinterpret_cast<const double*>(x)[k];
+        nb += llr_bad(xv, rule);
+        v = (F)xv;
       }
-      dst[i] = v + F(0);   // -0 -> +0 (equal values; see sign_xor)
     }
-    if (rule) llr_count(bad, b_);
+    dst[i] = v + F(0);   // -0 -> +0 (equal values; see sign_xor)
   }
+  llr_count(bad, nb);
 }
 
 // channel staging for the fused decoder: user LLRs [N][B] -> [group][variable position] 16-byte slots
@@ -700,7 +693,7 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
     __syncthreads();
     constexpr int kPer = P * G / 256;   // cells per thread, all loads issued before the LDS stores
     VT v[kPer];
-    bool b_ = false;
+    int nb = 0;
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
@@ -713,25 +706,25 @@ __global__ __launch_bounds__(256) void fl_stage_t(const void* x, int in_dtype, i
         if (vec) {
           v[it] = *reinterpret_cast<const VT*>(reinterpret_cast<const F*>(x) + k);
 #pragma unroll
-          for (int s = 0; s < N; ++s) b_ |= llr_bad(V::get(v[it], s), rule);
+          for (int s = 0; s < N; ++s) nb += llr_bad(V::get(v[it], s), rule);
         } else {
 #pragma unroll
           for (int s = 0; s < N; ++s)
             if (g * N + s < B) {
               if (in_dtype == kF32) {
                 const float xv = reinterpret_cast<const float*>(x)[k + s];
-                b_ |= llr_bad(xv, rule);
+                nb += llr_bad(xv, rule);
                 V::set(v[it], s, (F)xv);
               } else {
                 const double xv = reinterpret_cast<const double*>(x)[k + s];
-                b_ |= llr_bad(xv, rule);
+                nb += llr_bad(xv, rule);
                 V::set(v[it], s, (F)xv);
               }
             }
         }
       }
     }
-    if (rule) llr_count(bad, b_);
+    llr_count(bad, nb);
 #pragma unroll
     for (int it = 0; it < kPer; ++it) {
       const int i = fl_tid() + it * 256;
