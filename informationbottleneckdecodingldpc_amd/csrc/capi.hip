@@ -1156,9 +1156,12 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   // at most 16 waves per CU: with a second block per CU its waves issue behind the first block's
   // (oldest-first) and the per-block work counters cannot rebalance across blocks
   if (fl_occupancy(0, kind, precision, g->dcm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
-  h->grid_cn = std::min(bpc, 1024 / fl_block(0, kind, precision, g->dcm)) * g->num_cus;
+  // (A/B knob, read once here: IBL_FL_WAVES = waves per CU the per-pass grids may fill, default 16)
+  const char* fw = getenv("IBL_FL_WAVES");
+  const int wcap = std::max(16, fw ? atoi(fw) : 16) * 64;
+  h->grid_cn = std::min(bpc, wcap / fl_block(0, kind, precision, g->dcm)) * g->num_cus;
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
-  h->grid_vn = std::min(bpc, 1024 / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
+  h->grid_vn = std::min(bpc, wcap / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
   if ((rc = fused_setup(h))) return bail(rc);
   {  // degree-2 variable fold of the per-pass path (IBL_FL_FOLD=0 at create turns it off: A/B)
     const char* fe = getenv("IBL_FL_FOLD");

@@ -89,7 +89,7 @@ for s in $STEPS; do
         rc=$?; echo "line $name rc=$rc $(jf $O/line_$name.json)" >> $O/summary.txt; chk $rc line_$name
       done < ${LINES:-tools/lines_default.txt};;
     mrank)   # N>1 bench path rehearsed on one GPU: 2 ranks sharing cuda:0 over gloo
-      IBL_SHARE_DEVICE=1 IBL_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_2rank.json 2> $O/bench_2rank.err
+      IBL_SHARE_DEVICE=1 IBL_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline ${MRANK_ARGS:-} > $O/bench_2rank.json 2> $O/bench_2rank.err
       rc=$?; echo "mrank rc=$rc" >> $O/summary.txt; chk $rc mrank;;
     *) echo "unknown step $s" >> $O/summary.txt; exit 2;;
   esac
