@@ -71,14 +71,21 @@ def sq(out, config, paths):
         json.dump(doc, fh, indent=1)
 
 
+# float per-pass degree-2 fold (round 5): folded variables and check passes per decode (imax - 1; all but
+# the last fold) of the configs that run it
+FOLD = {"C5": (32399, 99)}
+
+
 def _alg(config, kname):
-    """Stored algorithmic (read, write) bytes per launch of a per-pass kernel."""
+    """Stored algorithmic (read, write) bytes per launch of a per-pass kernel (averaged over the decode's
+    launches: with the fold, all check passes but the last also read 2 channel rows per folded variable)."""
     E, N, B, w, _ = CONFIGS[config]
+    nf, ncn = FOLD.get(config, (0, 1))
     base = kname.split("::")[-1].split("<")[0]
     if base in ("ib_cn_fast", "fl_cn", "ib_cn_gen"):
-        return E * B * w, E * B * w
+        return (E + 2 * nf * (ncn - 1) / ncn) * B * w, E * B * w
     if base in ("ib_vn_fast", "fl_vn", "ib_vn_gen"):
-        return (E + N) * B * w, E * B * w
+        return (E - 2 * nf + N - nf) * B * w, (E - 2 * nf) * B * w
     return None
 
 
