@@ -98,6 +98,17 @@ int ibl_ib_path(const ibl_ib* h);
 int ibl_ib_set_path(ibl_ib* h, int32_t path);
 int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
 /*
+ * Small-batch kernels of the fast path (no reference counterpart; outputs identical to the other
+ * kernels).  The per-pass fast kernels give every wave one node x 1024 codewords, so a batch of a few
+ * codewords — the reference's DVB-S2 driver decodes msg_at_time = 2 (BER_simulation_OpenCL.py:71) —
+ * costs what B = 1024 costs; batches B <= max_b instead run kernels whose wave item is up to 64 nodes
+ * of one degree (lane = node) x 8 codewords.  Default max_b = 64 (IBL_SMALL_B in the environment when
+ * the decoder is created overrides it); 0 turns them off.  The fused on-chip path, when in use, ignores
+ * this.  IBL_EUNSUPPORTED if max_b > 0 and the decoder has no fast path.
+ */
+int ibl_ib_set_small_batch(ibl_ib* h, int32_t max_b);
+int ibl_ib_small_batch(const ibl_ib* h, int32_t* max_b);
+/*
  * Codewords per workgroup the fused kernel runs a batch of B with (no reference counterpart; results are
  * identical either way): 8, or 4 (half groups) when 2 * ceil(B / 8) workgroups fit the grid or the
  * environment IBL_FUSED_NCW=4 forces them and the half-group kernel fits the device; 0 when decodes do

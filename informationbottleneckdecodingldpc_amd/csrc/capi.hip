@@ -85,6 +85,9 @@ struct ibl_graph {
   // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable)
   int32_t *cn_info = nullptr, *vn_info = nullptr;
   int32_t cn_heavy = 0, vn_heavy = 0;
+  // small-batch kernels: tasks of up to 64 consecutive same-degree positions of cn_info / vn_info
+  int32_t *cn_task = nullptr, *vn_task = nullptr;
+  int32_t n_cn_task = 0, n_vn_task = 0;
 };
 
 namespace {
@@ -104,6 +107,19 @@ std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::ve
     if (deg[v] > kLightD) ++*heavy;
   }
   return info;
+}
+// {first position, count, degree, 0}: runs of at most 64 positions of one degree in a work order
+std::vector<int32_t> order_tasks(const std::vector<int32_t>& info) {
+  std::vector<int32_t> t;
+  const int32_t n = (int32_t)(info.size() / 4);
+  for (int32_t p = 0; p < n;) {
+    const int32_t d = info[4 * p + 2];
+    int32_t c = 0;
+    while (p + c < n && c < 64 && info[4 * (p + c) + 2] == d) ++c;
+    t.insert(t.end(), {p, c, d, 0});
+    p += c;
+  }
+  return t;
 }
 }  // namespace
 
@@ -178,6 +194,9 @@ struct ibl_ib {
   int32_t path = IBL_PATH_AUTO;
   bool fused_ok = false, f_half_ok = false;   // f_half_ok: the 4-codeword-group kernel is usable too
   int32_t f_ncw_forced = 0;                   // IBL_FUSED_NCW read once at create (A/B, tests), 0 = auto
+  // small-batch per-pass kernels (ib_*_small) for B <= small_b (0: off); LDS bytes per launch kind
+  int32_t small_b = 0;
+  size_t s_lds_cn = 0, s_lds_vn = 0, s_lds_dec = 0;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
@@ -291,11 +310,20 @@ int ibl_graph_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const int3
   if ((rc = dupload(&g->cn_start, cs.data(), n_c)) || (rc = dupload(&g->cn_deg, cd.data(), n_c)) ||
       (rc = dupload(&g->tgt_cn, tc.data(), E)) || (rc = dupload(&g->vn_start, vs.data(), n_v)) ||
       (rc = dupload(&g->vn_deg, vd.data(), n_v)) || (rc = dupload(&g->tgt_vn, tv.data(), E)) ||
-      (rc = dupload(&g->csr_cols, cols, E)) ||
-      (rc = dupload(&g->cn_info, work_order(cs, cd, &g->cn_heavy).data(), (size_t)n_c * 4)) ||
-      (rc = dupload(&g->vn_info, work_order(vs, vd, &g->vn_heavy).data(), (size_t)n_v * 4))) {
+      (rc = dupload(&g->csr_cols, cols, E))) {
     ibl_graph_destroy(g);
     return rc;
+  }
+  {
+    const std::vector<int32_t> ci = work_order(cs, cd, &g->cn_heavy), vi = work_order(vs, vd, &g->vn_heavy);
+    const std::vector<int32_t> ct = order_tasks(ci), vt = order_tasks(vi);
+    g->n_cn_task = (int32_t)(ct.size() / 4);
+    g->n_vn_task = (int32_t)(vt.size() / 4);
+    if ((rc = dupload(&g->cn_info, ci.data(), ci.size())) || (rc = dupload(&g->vn_info, vi.data(), vi.size())) ||
+        (rc = dupload(&g->cn_task, ct.data(), ct.size())) || (rc = dupload(&g->vn_task, vt.data(), vt.size()))) {
+      ibl_graph_destroy(g);
+      return rc;
+    }
   }
   *out = g;
   return IBL_OK;
@@ -316,7 +344,7 @@ void ibl_graph_destroy(ibl_graph* g) {
   (void)hipSetDevice(g->device);
   dfree(g->cn_start); dfree(g->cn_deg); dfree(g->tgt_cn);
   dfree(g->vn_start); dfree(g->vn_deg); dfree(g->tgt_vn); dfree(g->csr_cols);
-  dfree(g->cn_info); dfree(g->vn_info);
+  dfree(g->cn_info); dfree(g->vn_info); dfree(g->cn_task); dfree(g->vn_task);
   delete g;
 }
 
@@ -572,6 +600,16 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       return bail(fail(IBL_EHIP, std::string("fast-path kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill / scratch item): rebuild required"));
     if ((rc = ib_fused_setup(h))) return bail(rc);
+    // small-batch per-pass kernels: the fast path's tables without column images; used for B <= small_b
+    // (IBL_SMALL_B at create overrides the default, 0 turns them off)
+    if (h->cn_ncs == 0 && h->vn_ncs == 0) {
+      HIPCHK(ib_small_private_bytes(CM, VM, &priv, &kname));
+      const char* sb = getenv("IBL_SMALL_B");
+      h->small_b = priv == 0 ? (sb ? std::max(0, atoi(sb)) : kSmallBatchDefault) : 0;
+      h->s_lds_cn = (size_t)h->cn_nt * kRegion;
+      h->s_lds_vn = (size_t)h->vn_nt * kRegion;
+      h->s_lds_dec = (size_t)h->dec_nt * kRegion;
+    }
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
     if ((rc = dupload(&h->cn_lut, cn_lut, cn_len)) || (rc = dupload(&h->vn_lut, vn_lut, vn_len))) return bail(rc);
@@ -585,6 +623,21 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
 }
 
 int ibl_ib_path(const ibl_ib* h) { return h && h->fast ? 1 : 0; }
+
+int ibl_ib_set_small_batch(ibl_ib* h, int32_t max_b) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (max_b < 0) return fail(IBL_EINVAL, "max_b must be >= 0");
+  if (max_b > 0 && !(h->fast && h->cn_ncs == 0 && h->vn_ncs == 0 && h->s_lds_cn > 0))
+    return fail(IBL_EUNSUPPORTED, "the small-batch kernels need the fast path (T_ch = T_dec <= 16, degrees <= 16)");
+  h->small_b = max_b;
+  return IBL_OK;
+}
+
+int ibl_ib_small_batch(const ibl_ib* h, int32_t* max_b) {
+  if (!h || !max_b) return fail(IBL_EINVAL, "NULL argument");
+  *max_b = h->small_b;
+  return IBL_OK;
+}
 
 
 int ibl_ib_set_path(ibl_ib* h, int32_t path) {
@@ -702,6 +755,54 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
       f.dL = h->dL;
       HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_fused(f, h->CM, h->VM, grid, h->f_block, h->f_lds, s); }));
     }
+    return IBL_OK;
+  }
+  if (h->fast && B <= h->small_b) {
+    // small batch: (task, word) items, lane = node (ib_*_small); the pass schedule of the fast path
+    const int ldbb = h->ldb / 2, nwords = (B + 7) / 8;
+    HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
+    auto grid_of = [&](int ntask, size_t lds) {
+      const int per_cu = std::max(1, (int)(kLdsBytes / std::max<size_t>(lds, 1)));
+      const int need = (ntask * nwords + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
+      return std::max(1, std::min(need, per_cu * g->num_cus));
+    };
+    IbFastArgs cn{}, vn{};
+    cn.ch8 = vn.ch8 = h->ch8;
+    cn.info = g->cn_info; cn.task = g->cn_task; cn.n_tasks = g->n_cn_task; cn.tgt = g->tgt_cn; cn.out = h->vin;
+    vn.info = g->vn_info; vn.task = g->vn_task; vn.n_tasks = g->n_vn_task; vn.tgt = g->tgt_vn; vn.out = h->cin;
+    vn.in = h->vin;
+    cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.nwords = vn.nwords = nwords;
+    cn.ldb = vn.ldb = ldbb;
+    cn.B = vn.B = B;
+    cn.half = vn.half = h->T / 2;
+    cn.match = vn.match = h->match;
+    cn.nt = h->cn_nt; vn.nt = h->vn_nt;
+    std::memcpy(cn.fslot, h->cn_fslot, sizeof(cn.fslot));
+    std::memcpy(vn.fslot, h->vn_fslot, sizeof(vn.fslot));
+    const int gcn = grid_of(g->n_cn_task, h->s_lds_cn), gvn = grid_of(g->n_vn_task, h->s_lds_vn);
+    cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
+    HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
+    cn.gather = nullptr;
+    cn.in = h->cin;
+    for (int j = 1; j < I; ++j) {
+      const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+      vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
+      vn.gate = gate;
+      HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_small(vn, h->VM, gvn, h->s_lds_vn, s); }));
+      cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
+      cn.gate = gate;
+      cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
+    }
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    IbDecArgs dc{};
+    dc.vin = h->vin; dc.ch8 = h->ch8; dc.img = h->dec_img; dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype;
+    dc.nt = h->dec_nt; dc.n_nodes = g->n_v; dc.ldb = ldbb; dc.B = B;
+    dc.info = g->vn_info; dc.task = g->vn_task; dc.n_tasks = g->n_vn_task; dc.nwords = nwords;
+    const size_t esz = out_dtype == kU8 ? 1 : 4;
+    dc.aligned = ((B % 4) == 0 && ((uintptr_t)d_out % (4 * esz)) == 0) ? 1 : 0;
+    HIPCHK(launch_ib_dec_small(dc, grid_of(g->n_vn_task, h->s_lds_dec), h->s_lds_dec, s));
     return IBL_OK;
   }
   if (h->fast) {

@@ -91,6 +91,10 @@ struct IbFastArgs {
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
   uint64_t* trace;          // diagnostics (IBL_TRACE_WAVES): per wave {start clock, end clock, items}, else nullptr
+  // small-batch kernels (ib_*_small): tasks of up to 64 consecutive same-degree positions of `info`,
+  // {first position, count, degree, 0}; a wave item is (task, word), nwords = ceil(B / 8)
+  const int32_t* task;
+  int32_t n_tasks, nwords;
 };
 
 struct IbDecArgs {
@@ -102,6 +106,9 @@ struct IbDecArgs {
   const int32_t* iters;     // device scalar L (pass index of the decision tables)
   void* out;                // user output [N][B]
   int32_t out_dtype, nt, n_nodes, nchunks, ldb, B, aligned;
+  const int32_t* info;      // small-batch decision (ib_dec_small): variable work order and its tasks
+  const int32_t* task;
+  int32_t n_tasks, nwords;
 };
 
 // Fused on-chip IB decoder (short codes): a workgroup decodes 8 codewords at a time (one dword of
@@ -225,11 +232,19 @@ struct FlDecArgs {
 
 // launchers (defined in the .hip translation units, called by capi.hip)
 hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb, hipStream_t s);
+// writes the first ceil(B / 8) words of every row (the rest of a row is padding no output reads)
 hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s);
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s);
 int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for this max degree
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
+// small-batch per-pass kernels (B <= a few words): grid from the item count, block kSmallBlock
+constexpr int kSmallBlock = 256;
+constexpr int kSmallBatchDefault = 64;   // batches up to this many codewords take the small-batch kernels
+hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
+hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
+hipError_t launch_ib_dec_small(const IbDecArgs& a, int grid, size_t lds, hipStream_t s);
+hipError_t ib_small_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name);
 hipError_t ib_fast_occupancy(int which, int maxd, int block, size_t lds, int* blocks_per_cu);
 // Largest private (scratch) segment over the fast-path kernels a decoder of max degree maxd launches
 // (CN with and without gather, VN, decision); *name receives that kernel's name.

@@ -666,6 +666,164 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
   }
 }
 
+// ------------------------------------------------------- small-batch per-pass kernels
+// The fast kernels' wave item is one node x 512*W codewords: a batch of 2 codewords (the reference's
+// DVB-S2 driver, BER_simulation_OpenCL.py:71) leaves all but 2 of those codewords idle, and a pass costs
+// what a pass of B = 1024 costs. For batches of a few words a wave item is (task, word) instead: a task is
+// up to 64 consecutive positions of one degree in the pass's work order (lane = node, the fused kernel's
+// task shape), a word is codewords 8c..8c+7 (one dword of nibbles of every row), each lane gathering its
+// node's rows. Same table images, the fused kernel's node bodies on one dword (cn_word / vn_word /
+// dec_item), the same syndrome: outputs equal the fast path's bit for bit.
+template <int D, bool GATHER>
+__device__ __forceinline__ void cn_small_item(const IbFastArgs& a, uint32_t lane4, int st, int c, bool do_par,
+                                              bool& unsat) {
+  uint32_t in[D], o[D];
+  int tg[D];
+  const uint32_t off = 4u * (uint32_t)c;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const int e = st + j;
+    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
+    in[j] = *reinterpret_cast<const uint32_t*>(row + off);
+    tg[j] = a.tgt[e];
+    o[j] = 0;
+  }
+  if (do_par) {   // parity of (m < T/2) over the inputs, 8 codewords at once (see cn_compute)
+    const uint32_t bias = (uint32_t)(8 - a.half) * 0x11111111u;
+    uint32_t x = (D & 1) ? 0x88888888u : 0u;
+#pragma unroll
+    for (int j = 0; j < D; ++j) x ^= in[j] + bias;
+    if (x & 0x88888888u & valid_nib8(a.B - 8 * c)) unsat = true;
+  }
+  const uint32_t fbase = slot_off(a.fslot[D]);
+  if constexpr (D == 2) {
+    if (a.match) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        uint32_t t0[4], t1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
+          t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
+        }
+        o[0] |= pack4n(t0, g);
+        o[1] |= pack4n(t1, g);
+      }
+    } else {
+      o[0] = in[1];
+      o[1] = in[0];
+    }
+  } else {
+    const uint32_t cb[4] = {0, 0, 0, 0};   // no column-fetched inputs (the host requires ncs == 0)
+    cn_word<D>(lane4, in, fbase, cb, o);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
+}
+
+template <int D>
+__device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane4, int node, int st, int c) {
+  uint32_t in[D], o[D];
+  int tg[D];
+  const uint32_t off = 4u * (uint32_t)c;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)(st + j) * a.ldb + off);
+    tg[j] = a.tgt[st + j];
+    o[j] = 0;
+  }
+  const uint32_t chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + off);
+  if constexpr (D == 1) {
+    o[0] = chw;   // degree 1 forwards the channel value (kernels_template_irreg.cl:131-136)
+  } else {
+    const uint32_t cb[4] = {0, 0, 0, 0};
+    vn_word<D>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
+  }
+#pragma unroll
+  for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
+}
+
+// (task, word) items of a small-batch launch, dealt round-robin to the grid's waves; body(pos, c, d) runs
+// for the lanes whose position lies in the task (pos = this lane's position in the work order)
+template <class Args, class Body>
+__device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body) {
+  const int wpb = blockDim.x >> 6;
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  const int nw = gridDim.x * wpb, nitems = a.n_tasks * a.nwords;
+  for (int item = gw; item < nitems; item += nw) {
+    const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
+    const int c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
+    const int p0 = sload(a.task, 4 * t), cnt = sload(a.task, 4 * t + 1), d = sload(a.task, 4 * t + 2);
+    if (lane < cnt) body(p0 + lane, c, d);
+  }
+}
+
+template <int MAXD, bool GATHER>
+__global__ __launch_bounds__(kSmallBlock) void ib_cn_small(IbFastArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  if (!gate_open(a.gate, lane)) return;
+  lds_at_zero(lds);
+  stage_tables(lds, a.img, a.nt);
+  __syncthreads();
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  const bool do_par = !GATHER && a.unsat != nullptr;
+  bool unsat = false;
+  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int st = a.info[4 * pos + 1];
+    switch (d) {
+#define X(D) case D: if constexpr (D <= MAXD) cn_small_item<D, GATHER>(a, lane4, st, c, do_par, unsat); break;
+      IBL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  });
+  if (do_par && __ballot(unsat) != 0ull && lane == 0)
+    atomicOr(&a.unsat[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1)], 1);
+}
+
+template <int MAXD>
+__global__ __launch_bounds__(kSmallBlock) void ib_vn_small(IbFastArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  if (!gate_open(a.gate, lane)) return;
+  lds_at_zero(lds);
+  stage_tables(lds, a.img, a.nt);
+  __syncthreads();
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
+    switch (d) {
+      case 1: vn_small_item<1>(a, lane4, node, st, c); break;
+#define X(D) case D: if constexpr (D <= MAXD) vn_small_item<D>(a, lane4, node, st, c); break;
+      IBL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  });
+}
+
+__global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int L = __builtin_amdgcn_readfirstlane(*a.iters);
+  lds_at_zero(lds);
+  stage_tables(lds, a.img + (size_t)L * a.nt * 256, a.nt);
+  __syncthreads();
+  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
+    const uint32_t off = 4u * (uint32_t)c;
+    switch (d) {
+      case 1: dec_item<1>(a, lane4, node, st, off, 8 * c); break;
+#define X(D) case D: dec_item<D>(a, lane4, node, st, off, 8 * c); break;
+      IBL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  });
+}
+
 // ------------------------------------------------------------- fused on-chip decoder
 // For short codes (E * 4 B of messages plus the largest pass's table regions within the CU's LDS,
 // e.g. regular (3,6) N=8000: 96 KB + 32 KB), one workgroup decodes 8 codewords (a dword of 4-bit
@@ -1166,7 +1324,7 @@ __global__ void ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, 
 
 // ------------------------------------------- channel staging for the fast path (-> 4-bit nibbles)
 __global__ void ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes) {
-  const int words = ldb_bytes >> 2;
+  const int words = min(ldb_bytes >> 2, (B + 7) >> 3);   // padding words of a row are never output
   const size_t total = (size_t)n * words;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int row = (int)(i / words);
@@ -1336,7 +1494,7 @@ hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8
   return hipGetLastError();
 }
 hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s) {
-  const size_t total = (size_t)n * (ldb_bytes / 4);
+  const size_t total = (size_t)n * std::min(ldb_bytes / 4, (B + 7) / 8);
   const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
   hipLaunchKernelGGL(ib_stage4, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, ch4, ldb_bytes);
   return hipGetLastError();
@@ -1357,6 +1515,55 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
   return hipGetLastError();
 }
 int ib_fast_chunk(int maxd) { return maxd <= 8 ? chunkOf<8>() : chunkOf<16>(); }
+static bool ib_small_args_ok(const IbFastArgs& a, bool vn) {
+  return a.task && a.info && a.tgt && a.out && a.img && a.ch8 && (a.in || (!vn && a.gather)) && a.n_tasks >= 0 &&
+         a.nwords >= 1 && 4 * a.nwords <= a.ldb;
+}
+hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s) {
+  if (!ib_small_args_ok(a, false)) return hipErrorInvalidValue;
+  if (a.gather) {
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, true>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_small<16, true>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+  } else {
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, false>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_small<16, false>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s) {
+  if (!ib_small_args_ok(a, true)) return hipErrorInvalidValue;
+  if (maxd <= 8) hipLaunchKernelGGL(ib_vn_small<8>, dim3(grid), dim3(kSmallBlock), lds, s, a);
+  else hipLaunchKernelGGL(ib_vn_small<16>, dim3(grid), dim3(kSmallBlock), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_ib_dec_small(const IbDecArgs& a, int grid, size_t lds, hipStream_t s) {
+  if (!a.task || !a.info || !a.vin || !a.img || !a.out || a.nwords < 1 || 4 * a.nwords > a.ldb)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ib_dec_small, dim3(grid), dim3(kSmallBlock), lds, s, a);
+  return hipGetLastError();
+}
+hipError_t ib_small_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
+  const bool c8 = cn_maxd <= 8, v8 = vn_maxd <= 8;
+  const struct { const void* f; const char* n; } ks[] = {
+      {c8 ? (const void*)ib_cn_small<8, true> : (const void*)ib_cn_small<16, true>, "ib_cn_small<gather>"},
+      {c8 ? (const void*)ib_cn_small<8, false> : (const void*)ib_cn_small<16, false>, "ib_cn_small"},
+      {v8 ? (const void*)ib_vn_small<8> : (const void*)ib_vn_small<16>, "ib_vn_small"},
+      {(const void*)ib_dec_small, "ib_dec_small"}};
+  *bytes = 0;
+  *name = "";
+  for (const auto& k : ks) {
+    hipError_t e = hipFuncSetAttribute(k.f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e != hipSuccess) return e;
+    hipFuncAttributes fa;
+    e = hipFuncGetAttributes(&fa, k.f);
+    if (e != hipSuccess) return e;
+    if (fa.localSizeBytes > *bytes) {
+      *bytes = fa.localSizeBytes;
+      *name = k.n;
+    }
+  }
+  return hipSuccess;
+}
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s) {
   hipLaunchKernelGGL(ib_dec_fast, dim3(grid), dim3(block), lds, s, a);
   return hipGetLastError();

@@ -113,6 +113,17 @@ class IBDecoder:
         _lib.check(_lib.load().ibl_ib_path_in_use(self._h, ctypes.byref(f)), "ibl_ib_path_in_use")
         return bool(f.value)
 
+    @property
+    def small_batch(self) -> int:
+        """Largest batch the small-batch kernels decode (``ibl_ib_small_batch``; 0 = off)."""
+        n = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_ib_small_batch(self._h, ctypes.byref(n)), "ibl_ib_small_batch")
+        return int(n.value)
+
+    @small_batch.setter
+    def small_batch(self, max_b: int) -> None:
+        _lib.check(_lib.load().ibl_ib_set_small_batch(self._h, int(max_b)), "ibl_ib_set_small_batch")
+
     def fused_ncw(self, B: int) -> int:
         """Codewords per workgroup the fused kernel decodes a batch of ``B`` with (8, or 4 for half
         groups; 0 when the fused kernel is not in use) — ``ibl_ib_fused_ncw``."""

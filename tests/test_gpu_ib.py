@@ -25,9 +25,11 @@ def eng():
 
 
 def _run(eng, g_edges, tb, ch, match, early, out_dtype=torch.int32, ch_dtype=torch.int32, force_generic=False,
-         graph_obj=None, path="auto"):
+         graph_obj=None, path="auto", small_b=None, max_batch=None):
     G = graph_obj or eng.Graph(g_edges, DEV)
-    dec = eng.IBDecoder(G, tb, match, max_batch=ch.shape[1], force_generic=force_generic, path=path)
+    dec = eng.IBDecoder(G, tb, match, max_batch=max_batch or ch.shape[1], force_generic=force_generic, path=path)
+    if small_b is not None:
+        dec.small_batch = small_b
     it = torch.zeros(1, dtype=torch.int32, device=DEV)
     out = dec.decode(torch.from_numpy(ch).to(DEV).to(ch_dtype).contiguous(), out_dtype=out_dtype,
                      early_stop=early, iters=it)
@@ -49,6 +51,53 @@ def test_decode_ignores_diagnostic_environment(eng, dvb_H, monkeypatch):
     out, _, dec = _run(eng, g, tb, ch, True, False, path="passes")
     assert dec.fast_path
     np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("name,imax,B,match,early,ebn0", [
+    ("dvb", 6, 2, True, False, None),        # the reference DVB-S2 driver's msg_at_time
+    ("dvb", 20, 2, True, True, 3.0),         # converging: early stop before imax-1
+    ("dvb", 5, 33, False, True, None),       # ragged last word
+    ("dvb", 4, 130, True, False, None),      # 17 words, forced onto the small kernels
+    ("mixed16", 6, 9, False, True, None),    # every body of the MAXD=16 instantiations (degrees 2..16 / 1..16)
+    ("mixed8", 7, 64, True, True, 4.0)])     # MAXD=8 bodies with matching, converging
+def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H):
+    """The small-batch per-pass kernels (ib_*_small: wave item = up to 64 same-degree nodes x 8 codewords) and
+    the fast kernels (wave item = one node x 1024 codewords) both equal the oracle at small B, with the same
+    stop iteration; u8 and i32 in and out; a decoder sized for a larger max_batch (wider rows) too."""
+    H = {"dvb": lambda: dvb_H,
+         "mixed16": lambda: _mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15),
+         "mixed8": lambda: _mixed_code(np.array([3, 5, 6, 7, 8]), np.array([2, 3, 5, 6, 7, 8]), 500, seed=5)}[name]()
+    g = graph.build_graph(H)
+    G = eng.Graph(g, DEV)
+    if ebn0 is None:
+        tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=B + imax)
+        ch = np.random.default_rng(B).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    else:
+        q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
+        tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
+        ch = q.sample_all_zero(g.n_v, B, np.random.default_rng(B)).astype(np.int32)
+    ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
+    if ebn0 is not None and early:
+        assert ref_it < imax - 1
+    for small_b, mb, dt in ((1024, None, torch.int32), (1024, 5000, torch.uint8), (0, None, torch.int32)):
+        out, it, dec = _run(eng, g, tb, ch, match, early, path="passes", small_b=small_b, max_batch=mb,
+                            out_dtype=dt, ch_dtype=dt)
+        assert dec.fast_path and not dec.fused and dec.small_batch == small_b
+        assert it == ref_it, (small_b, mb)
+        np.testing.assert_array_equal(out, ref, err_msg=f"small_b={small_b} max_batch={mb}")
+
+
+def test_ib_small_batch_default_and_generic(eng, wlan_H):
+    """Default threshold 64; the generic path refuses the small-batch kernels."""
+    g = graph.build_graph(wlan_H)
+    G = eng.Graph(g, DEV)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 3)
+    assert eng.IBDecoder(G, tb, True, 16, path="passes").small_batch == 64
+    gen = eng.IBDecoder(G, tb, True, 16, force_generic=True)
+    assert gen.small_batch == 0
+    from informationbottleneckdecodingldpc_amd._lib import IBLError
+    with pytest.raises(IBLError):
+        gen.small_batch = 8
 
 
 CASES = [
