@@ -77,8 +77,8 @@ def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H):
         tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, imax)
         ch = q.sample_all_zero(g.n_v, B, np.random.default_rng(B)).astype(np.int32)
     ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
-    if ebn0 is not None and early:
-        assert ref_it < imax - 1
+    if name == "dvb" and ebn0 is not None and early:
+        assert ref_it < imax - 1            # the batch-global stop happens inside the loop
     for small_b, mb, dt in ((1024, None, torch.int32), (1024, 5000, torch.uint8), (0, None, torch.int32)):
         out, it, dec = _run(eng, g, tb, ch, match, early, path="passes", small_b=small_b, max_batch=mb,
                             out_dtype=dt, ch_dtype=dt)
