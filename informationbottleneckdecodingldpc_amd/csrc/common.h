@@ -240,7 +240,7 @@ int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
 // small-batch per-pass kernels (B <= a few words): grid from the item count, block kSmallBlock
 constexpr int kSmallBlock = 256;
-constexpr int kSmallBatchDefault = 64;   // batches up to this many codewords take the small-batch kernels
+constexpr int kSmallBatchDefault = 128;   // batches up to this many codewords take the small-batch kernels
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t launch_ib_dec_small(const IbDecArgs& a, int grid, size_t lds, hipStream_t s);

@@ -82,10 +82,21 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
 }
 
 // img: nreg regions x 256 dwords (row t*16+m, byte j = table 4R+j); replicated over the 32 banks
+// (LDS dword i = img[i >> 5]). Written as 16-byte units (unit u = dwords 4u..4u+3 = img[u >> 3]) by
+// consecutive lanes — conflict-free ds_write_b128 — four units per thread and round with their loads
+// issued together: a quarter of the store instructions of dword stores and a quarter of the dependent
+// load rounds (the 256-thread small-batch kernels staged 3 regions in ~7 us a region with dword stores).
 __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nreg) {
-  uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
-  const int n = nreg * (kRegion / 4);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  const int n = nreg * (kRegion / 16), bd = blockDim.x;
+  for (int u = threadIdx.x; u < n; u += 4 * bd) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = u + k * bd < n ? img[(u + k * bd) >> 3] : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (u + k * bd < n) l4[u + k * bd] = make_uint4(w[k], w[k], w[k], w[k]);
+  }
 }
 
 // column images: ncs tables x 16 columns x 2 dwords (entries t < 8, t >= 8) replicated for the 32
@@ -417,6 +428,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
   const uint32_t cw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + off);
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
+    if (cwb + 4 * g >= a.B) break;   // (wave-uniform in the small-batch kernel: every lane has the same word)
     uint32_t packed = 0;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -715,7 +727,9 @@ __device__ __forceinline__ void cn_small_item(const IbFastArgs& a, uint32_t lane
     }
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};   // no column-fetched inputs (the host requires ncs == 0)
-    cn_word<D>(lane4, in, fbase, cb, o);
+    // a word with at most 4 codewords of the batch left (B = 2: every word) computes nibbles 0..3 only
+    if (a.B - 8 * c <= 4) cn_word<D, 4>(lane4, in, fbase, cb, o);
+    else cn_word<D>(lane4, in, fbase, cb, o);
   }
 #pragma unroll
   for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
@@ -737,7 +751,8 @@ __device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane
     o[0] = chw;   // degree 1 forwards the channel value (kernels_template_irreg.cl:131-136)
   } else {
     const uint32_t cb[4] = {0, 0, 0, 0};
-    vn_word<D>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
+    if (a.B - 8 * c <= 4) vn_word<D, 4>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
+    else vn_word<D>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
   }
 #pragma unroll
   for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
