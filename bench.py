@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--early-stop", action="store_true",
                    help="batch-global early stop on (SURVEY §8(d)'s second line: at 1.0 dB unless --ebn0 is given); "
                         "IB decoders use LLR-derived tables (tables.llr_tables) so the batch can converge")
+    p.add_argument("--sub-batch", type=int, default=0,
+                   help="IB only: decode the batch as sequential sub-batches of this many codewords (one decoder sized "
+                        "for the sub-batch: its working set can stay in the 256-MiB Infinity Cache across passes)")
     p.add_argument("--batch-offset", type=int, default=0,
                    help="global batch index of rank 0's batch: rank r decodes global batch offset + r, whose channel "
                         "is Philox key 2 at counter (offset + r) * philox_blocks(N, B) (SURVEY H9)")
@@ -505,11 +508,23 @@ def main():
             match = True
         else:
             tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
-        dec = engine.IBDecoder(G, tb, match, B, path=a.path)
+        S = a.sub_batch if 0 < a.sub_batch < B else B
+        if B % S:
+            raise SystemExit("--sub-batch must divide the batch")
+        dec = engine.IBDecoder(G, tb, match, S, path=a.path)
         ch = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
         engine.channel_sample(ch, q.cdf_t_given_x_equals_zero, CH_SEED, ch_offset)
         out = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
-        run = lambda: dec.decode(ch, out=out, early_stop=early, iters=it_slot())     # noqa: E731
+        if S == B:
+            run = lambda: dec.decode(ch, out=out, early_stop=early, iters=it_slot())     # noqa: E731
+        else:   # contiguous [N][S] pieces, decoded one after another on the stream
+            chs = [ch[:, k * S:(k + 1) * S].contiguous() for k in range(B // S)]
+            outs = [torch.empty((n_v, S), dtype=torch.uint8, device=dev) for _ in chs]
+
+            def run():
+                for c_, o_ in zip(chs, outs):
+                    dec.decode(c_, out=o_, early_stop=early, iters=it_slot())
+                out.copy_(torch.cat(outs, dim=1))
         timing_on = lambda on: L.ibl_ib_timing(dec._h, int(on))    # noqa: E731
         timing_read_fn = L.ibl_ib_timing_read
         w, dtype = 1, "u8"
@@ -605,6 +620,7 @@ def main():
                                    f"{', early stop on (batch-global)' if early else ', fixed iterations'}",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "early_stop": early, "ebn0_db": a.ebn0, "batch_offset": a.batch_offset,
+                       "sub_batch": a.sub_batch or None,
                        "baseline_config": a.config or ("C4" if (a.code, a.kind, I) == ("dvbs2", "ib", 50) else None)},
             "hbm_gbps_algorithmic": round(value * moved / 1e9, 1),
             "bytes_per_codeword": int(round(moved)),

@@ -86,7 +86,16 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
 // consecutive lanes — conflict-free ds_write_b128 — four units per thread and round with their loads
 // issued together: a quarter of the store instructions of dword stores and a quarter of the dependent
 // load rounds (the 256-thread small-batch kernels staged 3 regions in ~7 us a region with dword stores).
+#ifndef IBL_STAGE_DWORD
+#define IBL_STAGE_DWORD 0   // 1: the round-4 dword-per-thread staging (A/B)
+#endif
 __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nreg) {
+  if constexpr (IBL_STAGE_DWORD) {
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
+    const int n = nreg * (kRegion / 4);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
+    return;
+  }
   uint4* l4 = reinterpret_cast<uint4*>(lds);
   const int n = nreg * (kRegion / 16), bd = blockDim.x;
   for (int u = threadIdx.x; u < n; u += 4 * bd) {

@@ -9,6 +9,8 @@ from informationbottleneckdecodingldpc_amd import _build  # noqa: E402
 
 VARIANTS = {
     "w1": ["IBL_W=1"],
+    # one dword per lane everywhere (rows padded to 512 codewords): the Infinity-Cache sub-batch experiment
+    "w1l1": ["IBL_W=1", "IBL_LIGHT_W=1"],
     "w1u": ["IBL_W=1", "IBL_CN_UNROLL=1"],
     "w2": ["IBL_W=2"],
     "w2u": ["IBL_W=2", "IBL_CN_UNROLL=1", "IBL_LB8=512"],
@@ -49,6 +51,8 @@ VARIANTS = {
     "nc22": ["IBL_NC_CN=2", "IBL_NC_VN=2", 'IBL_SCHED_FILE="ib_sched_nc22.inc"'],
     "nc33": ["IBL_NC_CN=3", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc33.inc"'],
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
+    # round-4 table staging (one dword store per thread and round) for the A/B of the 16-byte staging
+    "stagedw": ["IBL_STAGE_DWORD=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
     "ieeeon": [],
     # min-sum check node with the (min, second min) pair for every degree (the round-3 form)
