@@ -1033,9 +1033,10 @@ int fused_setup(ibl_float* h) {
 // reorders the variables of each degree for conflict-free dword slot reads (below).
 int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order) {
   const int64_t E = g->n_e;
-  std::vector<int32_t> tgt_vn((size_t)E);
-  if (hipMemcpy(tgt_vn.data(), g->tgt_vn, sizeof(int32_t) * (size_t)E, hipMemcpyDeviceToHost) != hipSuccess)
-    return fail(IBL_EHIP, "hipMemcpy failed");
+  // candidates the bank-order greedy scans per lane (IBL_FUSED_VWIN at create, A/B; default 256)
+  const char* vw = getenv("IBL_FUSED_VWIN");
+  const size_t vwin = (size_t)std::max(1, vw ? atoi(vw) : 256);
+  const std::vector<int32_t>& tgt_vn = g->h_tgt_vn;
   auto starts = [](const std::vector<int32_t>& deg) {
     std::vector<int64_t> st(deg.size() + 1, 0);
     for (size_t i = 0; i < deg.size(); ++i) st[i + 1] = st[i] + deg[i];
@@ -1082,7 +1083,7 @@ int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order) {
         for (int lane = 0; lane < 32 && !pool.empty(); ++lane) {
           size_t best = 0;
           int bestc = 1 << 30;
-          const size_t win = std::min<size_t>(pool.size(), 256);
+          const size_t win = std::min<size_t>(pool.size(), vwin);
           for (size_t c = 0; c < win && bestc > 0; ++c) {
             int col = 0;
             for (int k = 0; k < d && k <= kMaxD; ++k) col += (used[k] >> bank(pool[c], k)) & 1u;
