@@ -183,6 +183,14 @@ int ibl_float_path_in_use(const ibl_float* h, int32_t* fused);
  */
 int ibl_float_folded(const ibl_float* h, int32_t* n_folded);
 /*
+ * Small-batch kernels of the per-pass float path (no reference counterpart; outputs identical): batches
+ * B <= max_b run kernels whose wave item is up to 64 nodes of one degree (lane = node) x 4 fp32 / 2 fp64
+ * codewords instead of one node x 256 / 128 codewords; they do not fold.  Default max_b = 64
+ * (IBL_SMALL_B at create overrides it); 0 turns them off.  The fused path, when in use, ignores this.
+ */
+int ibl_float_set_small_batch(ibl_float* h, int32_t max_b);
+int ibl_float_small_batch(const ibl_float* h, int32_t* max_b);
+/*
  * Channel-LLR precondition check (no reference counterpart).  The staging step of every ibl_float_decode
  * counts the channel LLRs that break ibl_float_decode's precondition — NaN (min-sum); NaN, +-inf or
  * |x| > 354 (BP) — on the device, without a host sync.  This call synchronises `stream`, stores that count

@@ -31,6 +31,7 @@ EXPORTS = [
     "ibl_ib_destroy",
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
     "ibl_float_set_path", "ibl_float_path_in_use", "ibl_float_folded", "ibl_float_input_check",
+    "ibl_float_set_small_batch", "ibl_float_small_batch",
     "ibl_ib_timing", "ibl_ib_timing_read", "ibl_float_timing", "ibl_float_timing_read",
     "ibl_channel_sample",
     "ibl_encoder_create",
@@ -88,6 +89,8 @@ def load():
     L.ibl_float_set_path.argtypes = [_vp, _i32]
     L.ibl_float_path_in_use.argtypes = [_vp, ctypes.POINTER(_i32)]
     L.ibl_float_folded.argtypes = [_vp, ctypes.POINTER(_i32)]
+    L.ibl_float_set_small_batch.argtypes = [_vp, _i32]
+    L.ibl_float_small_batch.argtypes = [_vp, ctypes.POINTER(_i32)]
     L.ibl_float_input_check.argtypes = [_vp, ctypes.POINTER(_i32), _vp]
     for nm in ("ibl_ib_timing", "ibl_float_timing"):
         getattr(L, nm).argtypes = [_vp, _i32]

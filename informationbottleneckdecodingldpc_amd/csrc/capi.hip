@@ -219,6 +219,7 @@ struct ibl_float {
   int32_t *fold = nullptr, *vn_nodes = nullptr;
   int32_t n_vn_nodes = 0, n_folded = 0;
   int32_t* bad = nullptr;   // channel LLRs that violated the precondition since the last ibl_float_input_check
+  int32_t small_b = 0;      // small-batch kernels (fl_*_small) for B <= small_b (0: off)
   KTimer timer;
   // fused on-chip path (FlFusedArgs): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
@@ -1197,6 +1198,19 @@ int ibl_float_set_path(ibl_float* h, int32_t path) {
   return IBL_OK;
 }
 
+int ibl_float_set_small_batch(ibl_float* h, int32_t max_b) {
+  if (!h) return fail(IBL_EINVAL, "decoder is NULL");
+  if (max_b < 0) return fail(IBL_EINVAL, "max_b must be >= 0");
+  h->small_b = max_b;
+  return IBL_OK;
+}
+
+int ibl_float_small_batch(const ibl_float* h, int32_t* max_b) {
+  if (!h || !max_b) return fail(IBL_EINVAL, "NULL argument");
+  *max_b = h->small_b;
+  return IBL_OK;
+}
+
 int ibl_float_folded(const ibl_float* h, int32_t* n_folded) {
   if (!h || !n_folded) return fail(IBL_EINVAL, "NULL argument");
   *n_folded = h->n_folded;
@@ -1287,6 +1301,10 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
     if (priv != 0)
       return bail(fail(IBL_EHIP, std::string("float kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill): rebuild required"));
+    // small-batch kernels (IBL_SMALL_B at create overrides the default; off if they would need scratch)
+    HIPCHK(fl_small_private_bytes(kind, precision, g->dcm, g->dvm, &priv, &kname));
+    const char* sb = getenv("IBL_SMALL_B");
+    h->small_b = priv == 0 ? (sb ? std::max(0, atoi(sb)) : kFlSmallBatchDefault) : 0;
   }
   *out = h;
   return IBL_OK;
@@ -1359,6 +1377,47 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     return IBL_OK;
   }
   HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, rule, h->bad, s));
+  if (B <= h->small_b) {
+    // small batch: (task, word) items, lane = node (fl_*_small); the per-pass schedule without the fold
+    const int nwords = (B + cwl - 1) / cwl;
+    auto grid_of = [&](int ntask) {
+      const int need = (ntask * nwords + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
+      return std::max(1, std::min(need, 4 * g->num_cus));
+    };
+    FlArgs send{};
+    send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
+    send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;
+    HIPCHK(launch_fl_send(send, h->prec, s));
+    FlArgs cn{}, vn{};
+    cn.in = h->cin; cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.ch = h->chf;
+    vn.out = h->cin; vn.ch = h->chf; vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn;
+    cn.info = g->cn_info; cn.task = g->cn_task; cn.n_tasks = g->n_cn_task;
+    vn.info = g->vn_info; vn.task = g->vn_task; vn.n_tasks = g->n_vn_task;
+    cn.llr_max = vn.llr_max = h->llr_max;
+    cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
+    cn.nwords = vn.nwords = nwords;
+    cn.ldb = vn.ldb = h->ldb;
+    cn.B = vn.B = B;
+    const int gcn = grid_of(g->n_cn_task), gvn = grid_of(g->n_vn_task);
+    for (int j = 1; j < I; ++j) {
+      void* vb = (j & 1) ? h->vbuf1 : h->vbuf0;
+      cn.out = vb;
+      cn.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
+      cn.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn_small(cn, h->kind, h->prec, g->dcm, gcn, s); }));
+      if (j == I - 1) break;   // the last variable pass feeds no output (as below)
+      vn.in = vb;
+      vn.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+      HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn_small(vn, h->prec, g->dvm, gvn, s); }));
+    }
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
+    FlDecArgs dc{};
+    dc.vin0 = h->vbuf0; dc.vin1 = h->vbuf1; dc.ch = h->chf; dc.start = g->vn_start; dc.deg = g->vn_deg;
+    dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.n_nodes = g->n_v; dc.ldb = h->ldb; dc.B = B;
+    dc.info = g->vn_info; dc.task = g->vn_task; dc.n_tasks = g->n_vn_task; dc.nwords = nwords;
+    HIPCHK(launch_fl_dec_small(dc, h->prec, grid_of(g->n_vn_task), s));
+    return IBL_OK;
+  }
   FlArgs send{};
   send.ch = h->chf; send.out = h->cin;   // = cb[1] below
   send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;

@@ -192,6 +192,11 @@ struct FlArgs {
   void* fout;               // the next check pass's inbox (check order)
   int32_t fold_mode;
   const int32_t* nodes;     // variable pass: node list (the variables not folded), nullptr = 0..n_nodes-1
+  // small-batch kernels (fl_*_small): tasks of up to 64 consecutive same-degree positions of `info` (the IB
+  // fast path's work orders, {node, start, degree, 0}); a wave item is (task, word of Vec<F>::N codewords)
+  const int32_t* info;
+  const int32_t* task;
+  int32_t n_tasks, nwords;
 };
 constexpr int kFoldRec = 8;
 
@@ -228,6 +233,9 @@ struct FlDecArgs {
   const int32_t* iters;
   void* out;
   int32_t out_dtype, n_nodes, nchunks, ldb, B, aligned;
+  const int32_t* info;      // small-batch decision (fl_dec_small): variable work order and its tasks
+  const int32_t* task;
+  int32_t n_tasks, nwords;
 };
 
 // launchers (defined in the .hip translation units, called by capi.hip)
@@ -241,6 +249,7 @@ hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t ld
 // small-batch per-pass kernels (B <= a few words): grid from the item count, block kSmallBlock
 constexpr int kSmallBlock = 256;
 constexpr int kSmallBatchDefault = 128;   // batches up to this many codewords take the small-batch kernels
+constexpr int kFlSmallBatchDefault = 64;  // the float decoders' default threshold
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t launch_ib_dec_small(const IbDecArgs& a, int grid, size_t lds, hipStream_t s);
@@ -299,6 +308,11 @@ hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const in
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
+// small-batch float kernels (B <= a few words; lane = node): kSmallBlock threads per block
+hipError_t launch_fl_cn_small(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
+hipError_t launch_fl_vn_small(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
+hipError_t launch_fl_dec_small(const FlDecArgs& a, int prec, int grid, hipStream_t s);
+hipError_t fl_small_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, size_t* bytes, const char** name);
 hipError_t fl_occupancy(int which, int kind, int prec, int maxd, int* blocks_per_cu);
 // Largest private segment over the float kernels of (kind, prec, degrees); fused included when asked.
 hipError_t fl_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, bool fused, size_t* bytes,

@@ -765,6 +765,135 @@ __global__ void fl_send(FlArgs a) {
   }
 }
 
+// ------------------------------------------------------- small-batch per-pass kernels
+// As the IB small-batch kernels (ib_kernels.hip): the per-pass kernels' wave item is one node x 64 lanes x
+// Vec<F>::N codewords, so a batch of 2 costs a pass what B = 256 costs. For small batches a wave item is
+// (task, word): up to 64 consecutive same-degree positions of the work order (lane = node) x one word of
+// Vec<F>::N codewords, each lane gathering its node's 16-byte pieces of its rows. The node bodies are the
+// per-pass kernels' (fl_cn_body / fl_vn_body on the lane's N codewords, same operations in the same order),
+// so outputs equal the per-pass path's bit for bit. No fold (the small path runs every variable update).
+template <class Args, class Body>
+__device__ __forceinline__ void fl_small_items(const Args& a, int lane, Body&& body) {
+  const int wpb = fl_bdim() >> 6;
+  const int gw = __builtin_amdgcn_readfirstlane(fl_bid() * wpb + (fl_tid() >> 6));
+  const int nw = fl_gdim() * wpb, nitems = a.n_tasks * a.nwords;
+  for (int item = gw; item < nitems; item += nw) {
+    const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
+    const int c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
+    const int p0 = sload(a.task, 4 * t), cnt = sload(a.task, 4 * t + 1), d = sload(a.task, 4 * t + 2);
+    if (lane < cnt) body(p0 + lane, c, d);
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void fl_load_piece(const void* base, int ldb, int row, int cw0, F (&v)[Vec<F>::N]) {
+  using V = Vec<F>;
+  const typename V::T r = *reinterpret_cast<const typename V::T*>(reinterpret_cast<const F*>(base) + (size_t)row * ldb + cw0);
+#pragma unroll
+  for (int s = 0; s < V::N; ++s) v[s] = V::get(r, s);
+}
+
+template <int KIND, typename F, int D>
+__device__ __forceinline__ void fl_cn_small_item(const FlArgs& a, int st, int cw0, bool do_par, bool& unsat) {
+  constexpr int N = Vec<F>::N;
+  const F lm = (F)a.llr_max;
+  int tg[D];
+  F m[D][N];
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    tg[j] = a.tgt[st + j];
+    fl_load_piece<F>(a.in, a.ldb, st + j, cw0, m[j]);
+  }
+  if (do_par) {
+    const int valid = a.B - cw0;
+#pragma unroll
+    for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
+  }
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+    fl_store_to<F>(a.out, a.ldb, tg[w], cw0, o);
+  });
+}
+
+template <typename F, int D>
+__device__ __forceinline__ void fl_vn_small_item(const FlArgs& a, int node, int st, int cw0) {
+  constexpr int N = Vec<F>::N;
+  const F lm = (F)a.llr_max;
+  int tg[D];
+  F c[N], m[D][N];
+  fl_load_piece<F>(a.ch, a.ldb, node, cw0, c);
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    tg[j] = a.tgt[st + j];
+    fl_load_piece<F>(a.in, a.ldb, st + j, cw0, m[j]);
+  }
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+    fl_store_to<F>(a.out, a.ldb, tg[w], cw0, o);
+  });
+}
+
+template <int KIND, typename F, int MAXD>
+__global__ __launch_bounds__(kSmallBlock) void fl_cn_small(FlArgs a) {
+  const int lane = fl_tid() & 63;
+  if (!fl_gate(a.gate, lane)) return;
+  const bool do_par = a.unsat != nullptr;
+  bool unsat = false;
+  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int st = a.info[4 * pos + 1], cw0 = c * Vec<F>::N;
+    switch (d) {
+#define X(D) case D: if constexpr (D <= MAXD) fl_cn_small_item<KIND, F, D>(a, st, cw0, do_par, unsat); break;
+      FL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  });
+  if (do_par && __ballot(unsat) != 0ull && lane == 0)
+    atomicOr(&a.unsat[(fl_bid() * (fl_bdim() >> 6) + (fl_tid() >> 6)) & (kShards - 1)], 1);
+}
+
+template <typename F, int MAXD>
+__global__ __launch_bounds__(kSmallBlock) void fl_vn_small(FlArgs a) {
+  const int lane = fl_tid() & 63;
+  if (!fl_gate(a.gate, lane)) return;
+  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int node = a.info[4 * pos], st = a.info[4 * pos + 1], cw0 = c * Vec<F>::N;
+    switch (d) {
+      case 1: fl_vn_small_item<F, 1>(a, node, st, cw0); break;
+#define X(D) case D: if constexpr (D <= MAXD) fl_vn_small_item<F, D>(a, node, st, cw0); break;
+      FL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  });
+}
+
+// APP LLR of the small path: ch + every input in ascending edge order, unclamped (as fl_dec)
+template <typename F>
+__global__ __launch_bounds__(kSmallBlock) void fl_dec_small(FlDecArgs a) {
+  using V = Vec<F>;
+  constexpr int N = V::N;
+  const int L = __builtin_amdgcn_readfirstlane(*a.iters);
+  const void* vin = (L & 1) ? a.vin1 : a.vin0;
+  const int lane = fl_tid() & 63;
+  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int node = a.info[4 * pos], st = a.info[4 * pos + 1], cw0 = c * N;
+    F x[N], r[N];
+    fl_load_piece<F>(a.ch, a.ldb, node, cw0, x);
+    if (L > 0)
+      for (int v = 0; v < d; ++v) {
+        fl_load_piece<F>(vin, a.ldb, st + v, cw0, r);
+#pragma unroll
+        for (int s = 0; s < N; ++s) x[s] = x[s] + r[s];
+      }
+    const size_t o = (size_t)node * a.B + cw0;
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      if (cw0 + s >= a.B) break;
+      if (a.out_dtype == kF32) reinterpret_cast<float*>(a.out)[o + s] = (float)x[s];
+      else reinterpret_cast<double*>(a.out)[o + s] = (double)x[s];
+    }
+  });
+}
+
 // ------------------------------------------------------------ fused on-chip decoder
 // IBL_FL_CN64: full check tasks (64 nodes) run a body with the constant edge stride (A/B: 0 = off)
 #ifndef IBL_FL_CN64
@@ -1116,6 +1245,57 @@ hipError_t launch_fl_fused(const FlFusedArgs& a, int kind, int prec, int cmax, i
   void* p[] = {&args};
   return hipLaunchKernel(fl_fused_kernel(kind, prec, cmax, vmax), dim3(grid),
                          dim3(fl_fused_block(kind, prec, cmax)), p, lds, s);
+}
+
+static bool fl_small_ok(const FlArgs& a, bool vn) {
+  return a.info && a.task && a.in && a.out && a.tgt && (!vn || a.ch) && a.nwords >= 1 && a.ldb > 0 && a.B > 0;
+}
+template <int KIND>
+static const void* fl_cn_small_kernel(int prec, int maxd) {
+  if (prec == kF32) return maxd <= 8 ? (const void*)fl_cn_small<KIND, float, 8> : (const void*)fl_cn_small<KIND, float, 16>;
+  return maxd <= 8 ? (const void*)fl_cn_small<KIND, double, 8> : (const void*)fl_cn_small<KIND, double, 16>;
+}
+static const void* fl_small_kernel(int which, int kind, int prec, int maxd) {
+  if (which == 0) return kind == 0 ? fl_cn_small_kernel<0>(prec, maxd) : fl_cn_small_kernel<1>(prec, maxd);
+  if (which == 1)
+    return prec == kF32 ? (maxd <= 8 ? (const void*)fl_vn_small<float, 8> : (const void*)fl_vn_small<float, 16>)
+                        : (maxd <= 8 ? (const void*)fl_vn_small<double, 8> : (const void*)fl_vn_small<double, 16>);
+  return prec == kF32 ? (const void*)fl_dec_small<float> : (const void*)fl_dec_small<double>;
+}
+hipError_t launch_fl_cn_small(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s) {
+  if (!fl_small_ok(a, false)) return hipErrorInvalidValue;
+  FlArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_small_kernel(0, kind, prec, maxd), dim3(grid), dim3(kSmallBlock), p, 0, s);
+}
+hipError_t launch_fl_vn_small(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s) {
+  if (!fl_small_ok(a, true)) return hipErrorInvalidValue;
+  FlArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_small_kernel(1, 0, prec, maxd), dim3(grid), dim3(kSmallBlock), p, 0, s);
+}
+hipError_t launch_fl_dec_small(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
+  if (!a.info || !a.task || !a.vin0 || !a.vin1 || !a.ch || !a.out || a.nwords < 1) return hipErrorInvalidValue;
+  FlDecArgs args = a;
+  void* p[] = {&args};
+  return hipLaunchKernel(fl_small_kernel(2, 0, prec, 0), dim3(grid), dim3(kSmallBlock), p, 0, s);
+}
+hipError_t fl_small_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
+  const struct { const void* f; const char* n; } ks[] = {{fl_small_kernel(0, kind, prec, cn_maxd), "fl_cn_small"},
+                                                           {fl_small_kernel(1, kind, prec, vn_maxd), "fl_vn_small"},
+                                                           {fl_small_kernel(2, kind, prec, 0), "fl_dec_small"}};
+  *bytes = 0;
+  *name = "";
+  for (const auto& k : ks) {
+    hipFuncAttributes fa;
+    const hipError_t e = hipFuncGetAttributes(&fa, k.f);
+    if (e != hipSuccess) return e;
+    if (fa.localSizeBytes > *bytes) {
+      *bytes = fa.localSizeBytes;
+      *name = k.n;
+    }
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s) {

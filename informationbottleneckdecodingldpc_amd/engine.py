@@ -197,6 +197,17 @@ class FloatDecoder:
         return bool(f.value)
 
     @property
+    def small_batch(self) -> int:
+        """Largest batch the small-batch float kernels decode (``ibl_float_small_batch``; 0 = off)."""
+        n = ctypes.c_int32()
+        _lib.check(_lib.load().ibl_float_small_batch(self._h, ctypes.byref(n)), "ibl_float_small_batch")
+        return int(n.value)
+
+    @small_batch.setter
+    def small_batch(self, max_b: int) -> None:
+        _lib.check(_lib.load().ibl_float_set_small_batch(self._h, int(max_b)), "ibl_float_set_small_batch")
+
+    @property
     def folded(self) -> int:
         """Degree-2 variables the per-pass path folds into the check pass (``ibl_float_folded``)."""
         f = ctypes.c_int32()

@@ -524,3 +524,41 @@ def test_dropin_bp_raises_on_invalid_channel(wlan_H):
     llr[5, 2] = np.inf
     with pytest.raises(IBLError):
         bp.decode_OpenCL_belief_propagation(llr)
+
+
+# ------------------------------------------------------------------ small-batch per-pass kernels
+@pytest.mark.parametrize("prec", [torch.float32, torch.float64])
+@pytest.mark.parametrize("kind", [oracle.MINSUM, oracle.BP])
+@pytest.mark.parametrize("name,imax,B,early,ebn0", [
+    ("dvb", 12, 2, False, 1.0),        # the reference DVB-S2 driver's batch
+    ("dvb", 30, 33, True, 2.0),        # ragged last word, early stop
+    ("mixed", 6, 9, True, 2.0),        # every check degree 2..16, variable degree 1..16
+    ("wlan", 20, 70, True, 1.5)])      # forced onto the small kernels past the default threshold
+def test_float_small_batch_kernels(eng, prec, kind, name, imax, B, early, ebn0, wlan_H, dvb_H):
+    """The small-batch float kernels (fl_*_small: wave item = up to 64 same-degree nodes x one 16-byte word) give
+    the per-pass kernels' bits and stop iteration (small_b = 0 runs those, with the fold where it applies); fp64
+    min-sum also equals the oracle."""
+    H = {"dvb": dvb_H, "wlan": wlan_H}.get(name)
+    if H is None:
+        H = mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15)
+    g = graph.build_graph(H)
+    G = eng.Graph(g, DEV)
+    llr = _llrs(g, B, ebn0, seed=imax + 13 * B, quantised=True)
+    res = {}
+    for small_b in (1024, 0):
+        dec = eng.FloatDecoder(G, kind, imax, B, precision=prec, path="passes")
+        dec.small_batch = small_b
+        it = torch.zeros(1, dtype=torch.int32, device=DEV)
+        out = dec.decode(torch.from_numpy(llr).to(DEV).to(prec), early_stop=early, iters=it)
+        res[small_b] = (out.double().cpu().numpy(), int(it.item()))
+    assert res[1024][1] == res[0][1]
+    np.testing.assert_array_equal(res[1024][0], res[0][0])
+    if kind == oracle.MINSUM and prec == torch.float64:
+        ref, ref_it = oracle.float_decode(g, kind, imax, llr, early_stop=early, return_iters=True)
+        assert res[1024][1] == ref_it
+        np.testing.assert_array_equal(res[1024][0], ref)
+
+
+def test_float_small_batch_default(eng, dvb_H):
+    G = eng.Graph(graph.build_graph(dvb_H), DEV)
+    assert eng.FloatDecoder(G, 1, 5, 16).small_batch == 64
