@@ -575,7 +575,8 @@ def main():
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
     fused = dec.fused
-    folded = 0 if (a.kind == "ib" or fused) else dec.folded
+    small = (not fused) and B <= getattr(dec, "small_batch", 0) and (a.kind != "ib" or getattr(dec, "fast_path", False))
+    folded = 0 if (a.kind == "ib" or fused or small) else dec.folded   # the small-batch kernels do not fold
     stop_it = its[:a.steps].cpu().numpy() if a.steps > 0 else np.zeros(1, np.int32)
     fast = a.kind == "ib" and getattr(dec, "fast_path", False)
     # bytes per stored message / channel value as this build moves them: the IB fast path keeps 4-bit
@@ -616,7 +617,7 @@ def main():
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, "
                                    f"{('matching ' + ('on' if match else 'off') + ', ') if a.kind == 'ib' else ''}"
-                                   f"{'fused on-chip kernel' if fused else 'per-pass kernels'}"
+                                   f"{'fused on-chip kernel' if fused else ('small-batch per-pass kernels' if small else 'per-pass kernels')}"
                                    f"{', early stop on (batch-global)' if early else ', fixed iterations'}",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "early_stop": early, "ebn0_db": a.ebn0, "batch_offset": a.batch_offset,
