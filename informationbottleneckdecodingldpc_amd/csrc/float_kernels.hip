@@ -125,13 +125,45 @@ __device__ __forceinline__ bool fl_gate(const int32_t* gate, int lane) {
 // as soon as they are final, so only the D input rows are live in registers (WLAN's degree-11
 // variable nodes: 136 -> 85 VGPRs, +14 %); degrees <= 8 keep their outputs and store them together
 // at the end of the item, which measured 9 % faster on DVB-S2 (3.21 -> 2.93 ms per VN pass).
+// IBL_FL_NT = 1: the per-pass kernels' message / channel rows as nontemporal loads and stores (A/B; every
+// row is streamed once per pass, far beyond the caches at C5's B = 8192)
+#ifndef IBL_FL_NT
+#define IBL_FL_NT 0
+#endif
+template <typename F> struct NtVec;
+template <> struct NtVec<float> { typedef float T __attribute__((ext_vector_type(4))); };
+template <> struct NtVec<double> { typedef double T __attribute__((ext_vector_type(2))); };
+
+// one lane's piece (Vec<F>::N codewords) of a row
+template <typename F>
+__device__ __forceinline__ void fl_row_load(const F* p, F (&v)[Vec<F>::N]) {
+  using V = Vec<F>;
+  if constexpr (IBL_FL_NT) {
+    const typename NtVec<F>::T r = __builtin_nontemporal_load(reinterpret_cast<const typename NtVec<F>::T*>(p));
+#pragma unroll
+    for (int s = 0; s < V::N; ++s) v[s] = r[s];
+  } else {
+    const typename V::T r = *reinterpret_cast<const typename V::T*>(p);
+#pragma unroll
+    for (int s = 0; s < V::N; ++s) v[s] = V::get(r, s);
+  }
+}
+
 template <typename F>
 __device__ __forceinline__ void fl_store_to(void* base, int ldb, int row, int cw0, const F (&v)[Vec<F>::N]) {
   using V = Vec<F>;
-  typename V::T o;
+  F* p = reinterpret_cast<F*>(base) + (size_t)row * ldb + cw0;
+  if constexpr (IBL_FL_NT) {
+    typename NtVec<F>::T o;
 #pragma unroll
-  for (int s = 0; s < V::N; ++s) V::set(o, s, v[s]);
-  *reinterpret_cast<typename V::T*>(reinterpret_cast<F*>(base) + (size_t)row * ldb + cw0) = o;
+    for (int s = 0; s < V::N; ++s) o[s] = v[s];
+    __builtin_nontemporal_store(o, reinterpret_cast<typename NtVec<F>::T*>(p));
+  } else {
+    typename V::T o;
+#pragma unroll
+    for (int s = 0; s < V::N; ++s) V::set(o, s, v[s]);
+    *reinterpret_cast<typename V::T*>(p) = o;
+  }
 }
 template <typename F>
 __device__ __forceinline__ void fl_store(const FlArgs& a, int row, int cw0, const F (&v)[Vec<F>::N]) {
@@ -365,11 +397,7 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int node, int st, in
   for (int w = 0; w < D; ++w) tg[w] = sload(a.tgt, st + w);
   F m[D][N];
 #pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const typename V::T r = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
-#pragma unroll
-    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
-  }
+  for (int j = 0; j < D; ++j) fl_row_load<F>(src + (size_t)(st + j) * a.ldb + cw0, m[j]);
   // fold record: wave-uniform (scalar) positions, rows and variables; the channel rows load with the inputs
   int fp0 = -1, fp1 = -1, fd0 = 0, fd1 = 0;
   F c0[N], c1[N];
@@ -380,16 +408,8 @@ __device__ __forceinline__ void fl_cn_item(const FlArgs& a, int node, int st, in
     fd0 = sload(fr, 2);
     fd1 = sload(fr, 3);
     const F* ch = reinterpret_cast<const F*>(a.ch);
-    if (fp0 >= 0) {
-      const typename V::T r = *reinterpret_cast<const typename V::T*>(ch + (size_t)sload(fr, 4) * a.ldb + cw0);
-#pragma unroll
-      for (int s = 0; s < N; ++s) c0[s] = V::get(r, s);
-    }
-    if (fp1 >= 0) {
-      const typename V::T r = *reinterpret_cast<const typename V::T*>(ch + (size_t)sload(fr, 5) * a.ldb + cw0);
-#pragma unroll
-      for (int s = 0; s < N; ++s) c1[s] = V::get(r, s);
-    }
+    if (fp0 >= 0) fl_row_load<F>(ch + (size_t)sload(fr, 4) * a.ldb + cw0, c0);
+    if (fp1 >= 0) fl_row_load<F>(ch + (size_t)sload(fr, 5) * a.ldb + cw0, c1);
   }
   if (do_par) {
 #pragma unroll
@@ -466,17 +486,9 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 #pragma unroll
   for (int w = 0; w < D; ++w) tg[w] = sload(a.tgt, st + w);
   F c[N], m[D][N];
-  {
-    const typename V::T r = *reinterpret_cast<const typename V::T*>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0);
+  fl_row_load<F>(reinterpret_cast<const F*>(a.ch) + (size_t)node * a.ldb + cw0, c);
 #pragma unroll
-    for (int s = 0; s < N; ++s) c[s] = V::get(r, s);
-  }
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const typename V::T r = *reinterpret_cast<const typename V::T*>(src + (size_t)(st + j) * a.ldb + cw0);
-#pragma unroll
-    for (int s = 0; s < N; ++s) m[j][s] = V::get(r, s);
-  }
+  for (int j = 0; j < D; ++j) fl_row_load<F>(src + (size_t)(st + j) * a.ldb + cw0, m[j]);
   auto sink = [&](int w, const F (&o)[N]) __attribute__((always_inline)) { fl_store<F>(a, tg[w], cw0, o); };
   FlOut<F, D> ob;
   fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) { ob.put(w, o, sink); });
