@@ -125,10 +125,11 @@ __device__ __forceinline__ bool fl_gate(const int32_t* gate, int lane) {
 // as soon as they are final, so only the D input rows are live in registers (WLAN's degree-11
 // variable nodes: 136 -> 85 VGPRs, +14 %); degrees <= 8 keep their outputs and store them together
 // at the end of the item, which measured 9 % faster on DVB-S2 (3.21 -> 2.93 ms per VN pass).
-// IBL_FL_NT = 1: the per-pass kernels' message / channel rows as nontemporal loads and stores (A/B; every
-// row is streamed once per pass, far beyond the caches at C5's B = 8192)
+// IBL_FL_NT = 1: the per-pass kernels' message / channel rows as nontemporal loads and stores (every row is
+// streamed once per pass, far beyond the caches at C5's B = 8192). Same box, two repetitions
+// (profiles/r05_c5_nontemporal_ab.json): C5 16.37k / 16.39k cw/s vs 16.17k / 16.18k plain (fl_vn 2.05 vs 2.12 ms).
 #ifndef IBL_FL_NT
-#define IBL_FL_NT 0
+#define IBL_FL_NT 1
 #endif
 template <typename F> struct NtVec;
 template <> struct NtVec<float> { typedef float T __attribute__((ext_vector_type(4))); };

@@ -51,8 +51,8 @@ VARIANTS = {
     "nc22": ["IBL_NC_CN=2", "IBL_NC_VN=2", 'IBL_SCHED_FILE="ib_sched_nc22.inc"'],
     "nc33": ["IBL_NC_CN=3", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_nc33.inc"'],
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
-    # float per-pass rows as nontemporal loads / stores
-    "flnt": ["IBL_FL_NT=1"],
+    # float per-pass rows as plain loads / stores (the default is nontemporal since round 5)
+    "flplain": ["IBL_FL_NT=0"],
     # round-4 table staging (one dword store per thread and round) for the A/B of the 16-byte staging
     "stagedw": ["IBL_STAGE_DWORD=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
