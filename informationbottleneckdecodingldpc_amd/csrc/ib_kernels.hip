@@ -135,6 +135,10 @@ template <> struct RowVec<4> { typedef uint4 T; };
 // caches): 1 = nontemporal loads and stores of the variable pass's rows (the HBM-bound pass). The
 // check pass keeps plain accesses (its registers are at the cap). A/B on one box (tools/ab.sh, DVB-S2
 // B=8192, 2 reps): plain 163.3k cw/s (CN 0.4936 / VN 0.4936 ms), nontemporal 165.3k (0.4888 / 0.4860).
+// IBL_NT_CN: the same for the check pass's row loads (not pass 0's channel gather) and stores (A/B)
+#ifndef IBL_NT_CN
+#define IBL_NT_CN 0
+#endif
 #ifndef IBL_NT
 #define IBL_NT 1
 #endif
@@ -236,7 +240,7 @@ __device__ __forceinline__ void fetch_item(const IbFastArgs& a, int item, int la
   for (int j = 0; j < MAXD; ++j) {
     const int e = b.st + min(j, b.d - 1);
     const uint8_t* row = GATHER ? a.ch8 + (size_t)sload(a.gather, e) * a.ldb : a.in + (size_t)e * a.ldb;
-    load_row<W, VN && IBL_NT>(row + b.off, b.row[j]);
+    load_row<W, VN ? (bool)IBL_NT : ((bool)IBL_NT_CN && !GATHER)>(row + b.off, b.row[j]);
   }
   if (VN) {
     load_row<W, IBL_NT>(a.ch8 + (size_t)node * a.ldb + b.off, b.chw);
@@ -357,7 +361,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
     for (int w = 0; w < D; ++w) outw[w][i] = o[w];
   }
 #pragma unroll
-  for (int w = 0; w < D; ++w) store_row<W>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
+  for (int w = 0; w < D; ++w) store_row<W, (bool)IBL_NT_CN>(a.out + (size_t)trow[w] * (uint32_t)a.ldb + b.off, outw[w]);
 }
 
 // ---------------------------------------------------------------- variable node

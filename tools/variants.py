@@ -53,6 +53,8 @@ VARIANTS = {
     "s2": ["IBL_NC_CN=2", "IBL_NC_VN=3", 'IBL_SCHED_FILE="ib_sched_s2.inc"'],
     # float per-pass rows as plain loads / stores (the default is nontemporal since round 5)
     "flplain": ["IBL_FL_NT=0"],
+    # nontemporal check-pass rows (the variable pass's are nontemporal by default)
+    "ntcn": ["IBL_NT_CN=1"],
     # round-4 table staging (one dword store per thread and round) for the A/B of the 16-byte staging
     "stagedw": ["IBL_STAGE_DWORD=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
