@@ -148,3 +148,18 @@ def test_measured_lookup_ceiling_from_profile():
     import bench
     mc = bench.measured_lookup_ceiling()
     assert mc is not None and 20.0 < mc <= 32.0
+
+
+def test_bench_arguments(monkeypatch):
+    """Presets keep an explicit --batch-per-gpu; --early-stop moves the default Eb/N0 to SURVEY §8(d)'s 1.0 dB."""
+    import sys
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "C4", "--early-stop", "--batch-per-gpu", "32"])
+    a = bench.parse()
+    assert (a.code, a.kind, a.imax, a.batch_per_gpu, a.ebn0, a.early_stop) == ("dvbs2", "ib", 50, 32, 1.0, True)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "C5"])
+    a = bench.parse()
+    assert (a.kind, a.imax, a.batch_per_gpu, a.ebn0, a.early_stop, a.sub_batch, a.batch_offset) == \
+        ("bp", 100, 8192, 0.6, False, 0, 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "C1", "--ebn0", "2.5"])
+    a = bench.parse()
+    assert a.no_match and a.ebn0 == 2.5 and a.batch_per_gpu == 1000
