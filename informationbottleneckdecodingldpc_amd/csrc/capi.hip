@@ -1252,7 +1252,7 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   HIPCHK(hipSetDevice(g->device));
   auto* h = new ibl_float();
   h->g = g; h->kind = kind; h->imax = imax; h->prec = precision; h->max_batch = max_batch; h->llr_max = llr_max;
-  h->ldb = (max_batch + kChunk - 1) / kChunk * kChunk;
+  h->ldb = (max_batch + kFlRowPad - 1) / kFlRowPad * kFlRowPad;
   const size_t es = precision == kF32 ? 4 : 8;
   const size_t inbox = (size_t)g->n_e * h->ldb * es;
   int rc;
@@ -1437,7 +1437,8 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   vn.nodes = fold ? h->vn_nodes : nullptr;
   cn.llr_max = vn.llr_max = h->llr_max;
   cn.n_nodes = g->n_c; vn.n_nodes = fold ? h->n_vn_nodes : g->n_v;
-  cn.nchunks = vn.nchunks = nchunks;
+  cn.nchunks = nchunks;
+  vn.nchunks = (B + fl_vn_chunk(h->prec) - 1) / fl_vn_chunk(h->prec);
   cn.ldb = vn.ldb = h->ldb;
   cn.B = vn.B = B;
   for (int j = 1; j < I; ++j) {
