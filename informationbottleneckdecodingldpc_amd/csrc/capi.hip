@@ -1438,7 +1438,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   cn.llr_max = vn.llr_max = h->llr_max;
   cn.n_nodes = g->n_c; vn.n_nodes = fold ? h->n_vn_nodes : g->n_v;
   cn.nchunks = nchunks;
-  vn.nchunks = (B + fl_vn_chunk(h->prec) - 1) / fl_vn_chunk(h->prec);
+  vn.nchunks = (B + fl_vn_chunk(h->prec, g->dvm) - 1) / fl_vn_chunk(h->prec, g->dvm);
   cn.ldb = vn.ldb = h->ldb;
   cn.B = vn.B = B;
   for (int j = 1; j < I; ++j) {

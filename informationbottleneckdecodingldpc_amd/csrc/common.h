@@ -307,7 +307,7 @@ hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const in
                              int rule, int32_t* bad, hipStream_t s);
 hipError_t launch_fl_cn(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
-int fl_vn_chunk(int prec);   // codewords per wave item of the per-pass variable kernel
+int fl_vn_chunk(int prec, int maxd);   // codewords per wave item of the per-pass variable kernel
 constexpr int kFlRowPad = 512;   // float inbox rows are padded to this many codewords (every item shape fits)
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
 // small-batch float kernels (B <= a few words; lane = node): kSmallBlock threads per block

@@ -534,7 +534,10 @@ __device__ __forceinline__ void fl_vn_item2(const FlArgs& a, int node, int st, i
     fl_store_to<F>(a.out, a.ldb, tg[w], cw0 + N, hi);
   });
 }
-int fl_vn_chunk(int prec) { return 64 * (prec == kF32 ? 4 : 2) * (IBL_FL_VN2 ? 2 : 1); }
+// (the degree > 8 bodies keep one piece per lane: two would spill)
+template <int MAXD>
+constexpr bool fl_vn_wide() { return IBL_FL_VN2 && MAXD <= 8; }
+int fl_vn_chunk(int prec, int maxd) { return 64 * (prec == kF32 ? 4 : 2) * ((IBL_FL_VN2 && maxd <= 8) ? 2 : 1); }
 
 #define FL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 
@@ -601,7 +604,7 @@ template <typename F, int MAXD>
 __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
   const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
-  constexpr int CWL = Vec<F>::N * (IBL_FL_VN2 ? 2 : 1);
+  constexpr int CWL = Vec<F>::N * (fl_vn_wide<MAXD>() ? 2 : 1);
   constexpr int CH = 64 * CWL;
   __shared__ int ctr;
   if (fl_tid() == 0) ctr = 0;
@@ -615,7 +618,7 @@ __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
     const int node = a.nodes ? sload(a.nodes, pos) : pos;   // the fold's variable list skips folded nodes
     const int d = sload(a.deg, node), st = sload(a.start, node);
     const int cw0 = chunk * CH + lane * CWL;
-    if constexpr (IBL_FL_VN2) {
+    if constexpr (fl_vn_wide<MAXD>()) {
       switch (d) {
         case 1: fl_vn_item2<F, 1>(a, node, st, cw0); break;
 #define X(D) case D: if constexpr (D <= MAXD) fl_vn_item2<F, D>(a, node, st, cw0); break;
