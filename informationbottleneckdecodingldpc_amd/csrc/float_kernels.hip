@@ -501,6 +501,8 @@ __device__ __forceinline__ void fl_vn_item(const FlArgs& a, int node, int st, in
 #ifndef IBL_FL_VN2
 #define IBL_FL_VN2 0
 #endif
+// lane l takes the pieces at cw0 = chunk base + l*N and cw0 + 64*N: each load / store instruction covers 1 KiB
+// contiguous, two instructions a 2-KiB segment
 template <typename F, int D>
 __device__ __forceinline__ void fl_vn_item2(const FlArgs& a, int node, int st, int cw0) {
   constexpr int N = Vec<F>::N, N2 = 2 * N;
@@ -514,7 +516,7 @@ __device__ __forceinline__ void fl_vn_item2(const FlArgs& a, int node, int st, i
   {
     F lo[N], hi[N];
     fl_row_load<F>(ch + (size_t)node * a.ldb + cw0, lo);
-    fl_row_load<F>(ch + (size_t)node * a.ldb + cw0 + N, hi);
+    fl_row_load<F>(ch + (size_t)node * a.ldb + cw0 + 64 * N, hi);
 #pragma unroll
     for (int s = 0; s < N; ++s) { c[s] = lo[s]; c[N + s] = hi[s]; }
   }
@@ -522,7 +524,7 @@ __device__ __forceinline__ void fl_vn_item2(const FlArgs& a, int node, int st, i
   for (int j = 0; j < D; ++j) {
     F lo[N], hi[N];
     fl_row_load<F>(src + (size_t)(st + j) * a.ldb + cw0, lo);
-    fl_row_load<F>(src + (size_t)(st + j) * a.ldb + cw0 + N, hi);
+    fl_row_load<F>(src + (size_t)(st + j) * a.ldb + cw0 + 64 * N, hi);
 #pragma unroll
     for (int s = 0; s < N; ++s) { m[j][s] = lo[s]; m[j][N + s] = hi[s]; }
   }
@@ -531,7 +533,7 @@ __device__ __forceinline__ void fl_vn_item2(const FlArgs& a, int node, int st, i
 #pragma unroll
     for (int s = 0; s < N; ++s) { lo[s] = o[s]; hi[s] = o[N + s]; }
     fl_store_to<F>(a.out, a.ldb, tg[w], cw0, lo);
-    fl_store_to<F>(a.out, a.ldb, tg[w], cw0 + N, hi);
+    fl_store_to<F>(a.out, a.ldb, tg[w], cw0 + 64 * N, hi);
   });
 }
 // (the degree > 8 bodies keep one piece per lane: two would spill)
@@ -617,7 +619,7 @@ __global__ __launch_bounds__((fl_block_of<1, MAXD>())) void fl_vn(FlArgs a) {
     const int chunk = __builtin_amdgcn_readfirstlane(item - pos * a.nchunks);
     const int node = a.nodes ? sload(a.nodes, pos) : pos;   // the fold's variable list skips folded nodes
     const int d = sload(a.deg, node), st = sload(a.start, node);
-    const int cw0 = chunk * CH + lane * CWL;
+    const int cw0 = chunk * CH + lane * Vec<F>::N;   // (wide items: the second piece 64 * N further)
     if constexpr (fl_vn_wide<MAXD>()) {
       switch (d) {
         case 1: fl_vn_item2<F, 1>(a, node, st, cw0); break;
