@@ -1,0 +1,63 @@
+"""End-to-end BER-driver throughput on one GPU: `ber.run_ber` over the reference-named drop-in
+classes, as `DVB-S2/BER_simulation_OpenCL.py:95-121` drives them — per batch the device channel
+(`quantize_direct_OpenCL[_LLR]`), the decode (`decode_OpenCL[_belief_propagation]`, early stop on), the error
+count (`return_errors_all_zero`) and the host-side stop rule. One Eb/N0 point, a fixed number of batches
+(`max_blocks`), timed by the driver itself (`BERResult.seconds`: the point's loop, after the decoder is built).
+Compare `value` with the decode-only `bench.py` line of the same code and batch.
+
+  python tools/bench_ber.py [--batches K] [--cases c4,c4enc,c5]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(case, batches, B):
+    import torch
+    from informationbottleneckdecodingldpc_amd import codes, graph, tables
+    from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
+    from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
+    H = codes.dvbs2_structured(seed=0)
+    g = graph.build_graph(H)
+    ebn0 = 1.0
+    cfg = dict(EbN0_dB_start=ebn0, EbN0_dB_max_value=ebn0, target_error_rate=1.0, min_errors=10 ** 12,
+               msg_at_time=B, max_blocks=batches * B, sync_every=4, seed=2)
+    if case.startswith("c4"):
+        from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+            Discrete_LDPC_Decoder_class_irregular
+        q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
+        tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 50)
+        dec = Discrete_LDPC_Decoder_class_irregular(H, 50, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
+                                                    match="true")
+        cfg["encoded"] = case == "c4enc"
+        what = "IB T=16 i_max=50 (LLR-derived tables), Discrete_LDPC_Decoder_class_irregular"
+    else:
+        from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+        dec = BeliefPropagationDecoderClassIrregular(H, 100, 16, B)
+        cfg["llr_dtype"] = torch.float32
+        what = "BP fp32 i_max=100, BeliefPropagationDecoderClassIrregular"
+    r = run_ber(dec, BERConfig(**cfg))
+    sec = r.seconds[0]
+    return {"metric": "BER-driver decoded codewords/sec (run_ber: channel + decode + error count + stop rule)",
+            "case": case, "code": "DVB-S2-structured N=64800 R=1/2", "decoder": what,
+            "encoded_codewords": bool(cfg.get("encoded")), "ebn0_db": ebn0, "batch": B, "batches": r.blocks[0] // B,
+            "early_stop": True, "value": round(r.blocks[0] / sec, 1), "unit": "codewords/s",
+            "seconds": round(sec, 4), "errors": r.errors[0], "ber": float(r.BER_vector[0])}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--batches", type=int, default=8)
+    p.add_argument("--batch", type=int, default=8192)
+    p.add_argument("--cases", default="c4,c4enc,c5")
+    a = p.parse_args()
+    for c in a.cases.split(","):
+        print(json.dumps(run(c, a.batches if c != "c5" else max(2, a.batches // 4), a.batch)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
