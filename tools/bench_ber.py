@@ -24,8 +24,11 @@ def run(case, batches, B):
     H = codes.dvbs2_structured(seed=0)
     g = graph.build_graph(H)
     ebn0 = 1.0
+    # sync_every divides the batch count: run_ber decodes whole rounds of sync_every batches and discards the
+    # ones past the stop, which would otherwise be decoded inside the timed loop but not counted
+    sync = max(k for k in (4, 2, 1) if batches % k == 0)
     cfg = dict(EbN0_dB_start=ebn0, EbN0_dB_max_value=ebn0, target_error_rate=1.0, min_errors=10 ** 12,
-               msg_at_time=B, max_blocks=batches * B, sync_every=4, seed=2)
+               msg_at_time=B, max_blocks=batches * B, sync_every=sync, seed=2)
     if case.startswith("c4"):
         from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
             Discrete_LDPC_Decoder_class_irregular
@@ -56,7 +59,7 @@ def main():
     p.add_argument("--cases", default="c4,c4enc,c5")
     a = p.parse_args()
     for c in a.cases.split(","):
-        print(json.dumps(run(c, a.batches if c != "c5" else max(2, a.batches // 4), a.batch)), flush=True)
+        print(json.dumps(run(c, a.batches if c != "c5" else max(2, a.batches // 2), a.batch)), flush=True)
 
 
 if __name__ == "__main__":
