@@ -1381,7 +1381,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     // small batch: (task, word) items, lane = node (fl_*_small); the per-pass schedule without the fold
     const int nwords = (B + cwl - 1) / cwl;
     auto grid_of = [&](int ntask) {
-      const int need = (ntask * nwords + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
+      const int need = (ntask * nwords + kFlSmallBlock / 64 - 1) / (kFlSmallBlock / 64);
       return std::max(1, std::min(need, 4 * g->num_cus));
     };
     FlArgs send{};

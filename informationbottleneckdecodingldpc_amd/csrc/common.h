@@ -247,7 +247,11 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
 int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for this max degree
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
 // small-batch per-pass kernels (B <= a few words): grid from the item count, block kSmallBlock
-constexpr int kSmallBlock = 256;
+#ifndef IBL_SMALL_BLOCK
+#define IBL_SMALL_BLOCK 256
+#endif
+constexpr int kSmallBlock = IBL_SMALL_BLOCK;   // IB small-batch kernels
+constexpr int kFlSmallBlock = 256;             // float small-batch kernels (the degree-16 BP bodies need > 128 VGPRs)
 constexpr int kSmallBatchDefault = 128;   // batches up to this many codewords take the small-batch kernels
 constexpr int kFlSmallBatchDefault = 64;  // the float decoders' default threshold
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
@@ -310,7 +314,7 @@ hipError_t launch_fl_vn(const FlArgs& a, int prec, int maxd, int grid, hipStream
 int fl_vn_chunk(int prec, int maxd);   // codewords per wave item of the per-pass variable kernel
 constexpr int kFlRowPad = 512;   // float inbox rows are padded to this many codewords (every item shape fits)
 hipError_t launch_fl_dec(const FlDecArgs& a, int prec, int grid, hipStream_t s);
-// small-batch float kernels (B <= a few words; lane = node): kSmallBlock threads per block
+// small-batch float kernels (B <= a few words; lane = node): kFlSmallBlock threads per block
 hipError_t launch_fl_cn_small(const FlArgs& a, int kind, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_vn_small(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s);
 hipError_t launch_fl_dec_small(const FlDecArgs& a, int prec, int grid, hipStream_t s);

@@ -900,7 +900,7 @@ __device__ __forceinline__ void fl_vn_small_item(const FlArgs& a, int node, int 
 }
 
 template <int KIND, typename F, int MAXD>
-__global__ __launch_bounds__(kSmallBlock) void fl_cn_small(FlArgs a) {
+__global__ __launch_bounds__(kFlSmallBlock) void fl_cn_small(FlArgs a) {
   const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
   const bool do_par = a.unsat != nullptr;
@@ -919,7 +919,7 @@ __global__ __launch_bounds__(kSmallBlock) void fl_cn_small(FlArgs a) {
 }
 
 template <typename F, int MAXD>
-__global__ __launch_bounds__(kSmallBlock) void fl_vn_small(FlArgs a) {
+__global__ __launch_bounds__(kFlSmallBlock) void fl_vn_small(FlArgs a) {
   const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
   fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kSmallBlock) void fl_vn_small(FlArgs a) {
 
 // APP LLR of the small path: ch + every input in ascending edge order, unclamped (as fl_dec)
 template <typename F>
-__global__ __launch_bounds__(kSmallBlock) void fl_dec_small(FlDecArgs a) {
+__global__ __launch_bounds__(kFlSmallBlock) void fl_dec_small(FlDecArgs a) {
   using V = Vec<F>;
   constexpr int N = V::N;
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
@@ -1334,19 +1334,19 @@ hipError_t launch_fl_cn_small(const FlArgs& a, int kind, int prec, int maxd, int
   if (!fl_small_ok(a, false)) return hipErrorInvalidValue;
   FlArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_small_kernel(0, kind, prec, maxd), dim3(grid), dim3(kSmallBlock), p, 0, s);
+  return hipLaunchKernel(fl_small_kernel(0, kind, prec, maxd), dim3(grid), dim3(kFlSmallBlock), p, 0, s);
 }
 hipError_t launch_fl_vn_small(const FlArgs& a, int prec, int maxd, int grid, hipStream_t s) {
   if (!fl_small_ok(a, true)) return hipErrorInvalidValue;
   FlArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_small_kernel(1, 0, prec, maxd), dim3(grid), dim3(kSmallBlock), p, 0, s);
+  return hipLaunchKernel(fl_small_kernel(1, 0, prec, maxd), dim3(grid), dim3(kFlSmallBlock), p, 0, s);
 }
 hipError_t launch_fl_dec_small(const FlDecArgs& a, int prec, int grid, hipStream_t s) {
   if (!a.info || !a.task || !a.vin0 || !a.vin1 || !a.ch || !a.out || a.nwords < 1) return hipErrorInvalidValue;
   FlDecArgs args = a;
   void* p[] = {&args};
-  return hipLaunchKernel(fl_small_kernel(2, 0, prec, 0), dim3(grid), dim3(kSmallBlock), p, 0, s);
+  return hipLaunchKernel(fl_small_kernel(2, 0, prec, 0), dim3(grid), dim3(kFlSmallBlock), p, 0, s);
 }
 hipError_t fl_small_private_bytes(int kind, int prec, int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {
   const struct { const void* f; const char* n; } ks[] = {{fl_small_kernel(0, kind, prec, cn_maxd), "fl_cn_small"},
