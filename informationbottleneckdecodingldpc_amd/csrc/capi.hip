@@ -764,7 +764,8 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     auto grid_of = [&](int ntask, size_t lds) {
       const int per_cu = std::max(1, (int)(kLdsBytes / std::max<size_t>(lds, 1)));
-      const int need = (ntask * nwords + kSmallBlock / 64 - 1) / (kSmallBlock / 64);
+      const int wpb = small_block(nwords) / 64;
+      const int need = (ntask * nwords + wpb - 1) / wpb;
       return std::max(1, std::min(need, per_cu * g->num_cus));
     };
     IbFastArgs cn{}, vn{};

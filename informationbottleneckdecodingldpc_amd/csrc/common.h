@@ -247,10 +247,11 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
 int ib_fast_chunk(int maxd);  // codewords per wave item of the CN/VN kernel for this max degree
 hipError_t launch_ib_dec_fast(const IbDecArgs& a, int grid, int block, size_t lds, hipStream_t s);
 // small-batch per-pass kernels (B <= a few words): grid from the item count, block kSmallBlock
-#ifndef IBL_SMALL_BLOCK
-#define IBL_SMALL_BLOCK 256
-#endif
-constexpr int kSmallBlock = IBL_SMALL_BLOCK;   // IB small-batch kernels
+// IB small-batch kernels: built for blocks of up to 1024 threads, launched with small_block(nwords) threads
+constexpr int kSmallBlock = 1024;
+// block size by words per row (same box, DVB-S2 i_max = 50, profiles/r05_ib_small_block_ab.json): one word
+// (B <= 8) 256 threads — more blocks stage their tables in parallel; up to 8 words 512; more 1024
+__host__ __device__ constexpr int small_block(int nwords) { return nwords <= 1 ? 256 : (nwords <= 8 ? 512 : 1024); }
 constexpr int kFlSmallBlock = 256;             // float small-batch kernels (the degree-16 BP bodies need > 128 VGPRs)
 constexpr int kSmallBatchDefault = 128;   // batches up to this many codewords take the small-batch kernels
 constexpr int kFlSmallBatchDefault = 64;  // the float decoders' default threshold

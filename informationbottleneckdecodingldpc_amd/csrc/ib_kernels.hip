@@ -1550,24 +1550,24 @@ static bool ib_small_args_ok(const IbFastArgs& a, bool vn) {
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s) {
   if (!ib_small_args_ok(a, false)) return hipErrorInvalidValue;
   if (a.gather) {
-    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, true>), dim3(grid), dim3(kSmallBlock), lds, s, a);
-    else hipLaunchKernelGGL((ib_cn_small<16, true>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, true>), dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_small<16, true>), dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
   } else {
-    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, false>), dim3(grid), dim3(kSmallBlock), lds, s, a);
-    else hipLaunchKernelGGL((ib_cn_small<16, false>), dim3(grid), dim3(kSmallBlock), lds, s, a);
+    if (maxd <= 8) hipLaunchKernelGGL((ib_cn_small<8, false>), dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
+    else hipLaunchKernelGGL((ib_cn_small<16, false>), dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
   }
   return hipGetLastError();
 }
 hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s) {
   if (!ib_small_args_ok(a, true)) return hipErrorInvalidValue;
-  if (maxd <= 8) hipLaunchKernelGGL(ib_vn_small<8>, dim3(grid), dim3(kSmallBlock), lds, s, a);
-  else hipLaunchKernelGGL(ib_vn_small<16>, dim3(grid), dim3(kSmallBlock), lds, s, a);
+  if (maxd <= 8) hipLaunchKernelGGL(ib_vn_small<8>, dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
+  else hipLaunchKernelGGL(ib_vn_small<16>, dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
   return hipGetLastError();
 }
 hipError_t launch_ib_dec_small(const IbDecArgs& a, int grid, size_t lds, hipStream_t s) {
   if (!a.task || !a.info || !a.vin || !a.img || !a.out || a.nwords < 1 || 4 * a.nwords > a.ldb)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ib_dec_small, dim3(grid), dim3(kSmallBlock), lds, s, a);
+  hipLaunchKernelGGL(ib_dec_small, dim3(grid), dim3(small_block(a.nwords)), lds, s, a);
   return hipGetLastError();
 }
 hipError_t ib_small_private_bytes(int cn_maxd, int vn_maxd, size_t* bytes, const char** name) {

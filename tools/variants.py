@@ -57,9 +57,6 @@ VARIANTS = {
     "ntcn": ["IBL_NT_CN=1"],
     # float variable items over 2-KiB row segments (two 16-byte pieces per lane)
     "flvn2": ["IBL_FL_VN2=1"],
-    # small-batch kernels in 1024-thread blocks (fewer blocks, each stages its tables 4x faster)
-    "sb1024": ["IBL_SMALL_BLOCK=1024"],
-    "sb512": ["IBL_SMALL_BLOCK=512"],
     # round-4 table staging (one dword store per thread and round) for the A/B of the 16-byte staging
     "stagedw": ["IBL_STAGE_DWORD=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
