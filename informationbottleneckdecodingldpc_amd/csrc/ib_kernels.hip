@@ -70,7 +70,24 @@ __device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
 }
 
 // column term of a lookup: (m << 7) | 4*(lane & 31); the row term of t is t << 11 (see kRegion)
-__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) { return (m << 7) | lane4; }
+// IBL_COLCONST (timing bound only, wrong results; tools/variants.py colconst): every column term is the
+// lane's constant, i.e. the column terms cost no VALU while the LDS reads and row chains stay — the
+// most byte-placed (v_perm_b32) column terms could save.
+#ifndef IBL_COLCONST
+#define IBL_COLCONST 0
+#endif
+__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
+  if constexpr (IBL_COLCONST) return lane4;
+  return (m << 7) | lane4;
+}
+// keeps the input words of a body live when IBL_COLCONST leaves some of them unread
+template <int D>
+__device__ __forceinline__ void colconst_keep(const uint32_t (&in)[D]) {
+  if constexpr (IBL_COLCONST) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) asm volatile("" ::"v"(in[j]));
+  }
+}
 
 __device__ __forceinline__ uint32_t valid_mask4(int remaining) {
   return remaining >= 4 ? 0xFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
@@ -291,6 +308,7 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 template <int D, int NCW = 8>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
+  colconst_keep(in);
 #pragma unroll 1
   for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
 }
@@ -372,6 +390,7 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 template <int D, int NCW = 8>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
+  colconst_keep(in);
 #pragma unroll 1
   for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
@@ -879,6 +898,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
 template <int D, int NCW>
 __device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
+  colconst_keep(in);
   if constexpr (IBL_FUSED_UNROLL && D <= 6) {
 #pragma unroll
     for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, o, k0);
@@ -889,6 +909,7 @@ __device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&i
 template <int D, int NCW>
 __device__ __forceinline__ void fused_vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw, uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
+  colconst_keep(in);
   if constexpr (IBL_FUSED_UNROLL && D <= 4) {
 #pragma unroll
     for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);
