@@ -385,7 +385,9 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
 }
 
 // LDS bytes of a fast CN / VN launch: table regions, column images, the 2 work counters
-size_t fast_lds(int nt, int ncs) { return (size_t)regions_of(nt) * kRegion + (size_t)ncs * kColImg + 64; }
+size_t fast_lds(int nt, int ncs) {
+  return (size_t)regions_of(nt) * kRegion + (size_t)ncs * kColImg + 64 + kColPermSlack;
+}
 
 // One pass's column images (colf): per image slot, 16 columns m x {entries t = 0..7, t = 8..15} as nibbles
 void append_cols(std::vector<uint32_t>& img, const std::vector<Table>& tbs, const std::vector<int>& slots) {

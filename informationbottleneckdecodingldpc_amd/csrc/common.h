@@ -35,6 +35,14 @@ constexpr int kTbl = 8192;        // LDS bytes per IB lookup table (replicated o
 // t*16+m, bank lane&31 holds entry (t, m) of table `slot`, so a lookup address is
 // (t << 11) | (m << 7) | 4*(lane&31) + slot_off(slot) with the slot in the DS immediate.
 constexpr int kRegion = 4 * kTbl;
+// IBL_COLPERM (timing A/B only, wrong results; tools/variants.py colperm): column terms as one
+// v_perm_b32 from nibble-spread words (column stride 256 B, row stride 4 KiB) without the 64-KiB table
+// layout it needs: the lookups read the current layout at those addresses (same banks, so the same LDS
+// cycles); the per-pass launches get one spare region so every address stays inside the allocation.
+#ifndef IBL_COLPERM
+#define IBL_COLPERM 0
+#endif
+constexpr int kColPermSlack = IBL_COLPERM ? kRegion : 0;
 __host__ __device__ constexpr uint32_t slot_off(int s) { return (uint32_t)(s >> 2) * kRegion + (uint32_t)(s & 3); }
 constexpr int regions_of(int nt) { return (nt + 3) >> 2; }
 // Column images (tools/gen_sched.py "Column fetches"): the last cn_ncols(D) / vn_ncols(D) inputs of a

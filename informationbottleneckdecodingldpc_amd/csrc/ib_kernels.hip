@@ -44,7 +44,10 @@ __device__ __forceinline__ uint32_t lu(uint32_t x, uint32_t c) {
 // shift + separate ORs (3 ops for the 2 lookups that read each prefix value P_w).
 __device__ __forceinline__ uint32_t luc(uint32_t t, uint32_t q, uint32_t c) {
   uint32_t x;
-  asm("v_lshl_or_b32 %0, %1, 11, %2" : "=v"(x) : "v"(t), "v"(q));
+  if constexpr (IBL_COLPERM)
+    asm("v_lshl_or_b32 %0, %1, 12, %2" : "=v"(x) : "v"(t), "v"(q));
+  else
+    asm("v_lshl_or_b32 %0, %1, 11, %2" : "=v"(x) : "v"(t), "v"(q));
   return *(lds8_t*)(size_t)(x + c);
 }
 // Column fetch (tools/gen_sched.py, "Column fetches"): column T(., m) of one table as 16 nibbles
@@ -70,24 +73,7 @@ __device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
 }
 
 // column term of a lookup: (m << 7) | 4*(lane & 31); the row term of t is t << 11 (see kRegion)
-// IBL_COLCONST (timing bound only, wrong results; tools/variants.py colconst): every column term is the
-// lane's constant, i.e. the column terms cost no VALU while the LDS reads and row chains stay — the
-// most byte-placed (v_perm_b32) column terms could save.
-#ifndef IBL_COLCONST
-#define IBL_COLCONST 0
-#endif
-__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) {
-  if constexpr (IBL_COLCONST) return lane4;
-  return (m << 7) | lane4;
-}
-// keeps the input words of a body live when IBL_COLCONST leaves some of them unread
-template <int D>
-__device__ __forceinline__ void colconst_keep(const uint32_t (&in)[D]) {
-  if constexpr (IBL_COLCONST) {
-#pragma unroll
-    for (int j = 0; j < D; ++j) asm volatile("" ::"v"(in[j]));
-  }
-}
+__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) { return (m << 7) | lane4; }
 
 __device__ __forceinline__ uint32_t valid_mask4(int remaining) {
   return remaining >= 4 ? 0xFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
@@ -137,6 +123,16 @@ __device__ __forceinline__ void stage_cols(uint8_t* dst, const uint32_t* cimg, i
 // codeword c in nibble (c & 1) of byte c/2. A lane owns 8*W consecutive codewords = W dwords of
 // each row (W = rowW<MAXD>()), a wave item = one node x 512*W codewords (256*W-B row segments).
 __device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
+// column term of codeword k of input word w (the generated schedules' form). IBL_COLPERM: one v_perm_b32
+// per codeword from the word's even / odd nibbles spread to bytes (w & 0x0F0F0F0F, (w >> 4) & 0x0F0F0F0F,
+// shared by the codewords of a group): byte 0 and bytes 2-3 from the lane term, byte 1 = the nibble.
+__device__ __forceinline__ uint32_t colq(uint32_t w, int k, uint32_t lane4) {
+  if constexpr (IBL_COLPERM) {
+    const uint32_t src = (k & 1) ? ((w >> 4) & 0x0F0F0F0Fu) : (w & 0x0F0F0F0Fu);
+    return __builtin_amdgcn_perm(src, lane4, 0x03020000u | ((4u + (uint32_t)(k >> 1)) << 8));
+  }
+  return qidx(nib(w, k), lane4);
+}
 
 // all-ones nibbles for the codewords of a word that lie inside the batch
 __device__ __forceinline__ uint32_t valid_nib8(int remaining) {
@@ -308,7 +304,6 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 template <int D, int NCW = 8>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
-  colconst_keep(in);
 #pragma unroll 1
   for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
 }
@@ -390,7 +385,6 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 template <int D, int NCW = 8>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
-  colconst_keep(in);
 #pragma unroll 1
   for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
@@ -898,7 +892,6 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
 template <int D, int NCW>
 __device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
-  colconst_keep(in);
   if constexpr (IBL_FUSED_UNROLL && D <= 6) {
 #pragma unroll
     for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, o, k0);
@@ -909,7 +902,6 @@ __device__ __forceinline__ void fused_cn_word(uint32_t lane4, const uint32_t (&i
 template <int D, int NCW>
 __device__ __forceinline__ void fused_vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw, uint32_t fbase,
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
-  colconst_keep(in);
   if constexpr (IBL_FUSED_UNROLL && D <= 4) {
 #pragma unroll
     for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);

@@ -133,7 +133,7 @@ def emit_body(kind, D, S, L, NC):
     for j in u8_in:
         for s in range(S):
             base = "lane4f" if j == D - 1 else "lane4"
-            lines.append(f"  const uint32_t q{j}_{s} = qidx(nib(in[{j}], k0 + {s}), {base});")
+            lines.append(f"  const uint32_t q{j}_{s} = colq(in[{j}], k0 + {s}, {base});")
     for j in col_in:
         for s in range(S):
             lines.append(f"  const uint64_t C{j}_{s} = colf(nib(in[{j}], k0 + {s}), cb[{j - (D - NC)}]);")

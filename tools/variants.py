@@ -65,8 +65,8 @@ VARIANTS = {
     "msps0": ["IBL_MS_PS=0"],
     # fused float check tasks without the constant-stride body for full tasks
     "cn64off": ["IBL_FL_CN64=0"],
-    # timing bound (wrong results): column terms without VALU -- the most v_perm_b32 column terms could save
-    "colconst": ["IBL_COLCONST=1"],
+    # timing A/B (wrong results): v_perm_b32 column terms at their real instruction cost (common.h IBL_COLPERM)
+    "colperm": ["IBL_COLPERM=1"],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
