@@ -363,8 +363,9 @@ Table make_table(int T, const std::function<int(int, int)>& f) {
   return tb;
 }
 
-// One pass's tables as 32-KiB LDS regions (kRegion): nreg x 256 dwords, dword (t*16+m) of region R
-// holds entry (t, m) of table 4R+j in byte j (slot_off). Unused slots of the last region are 0.
+// One pass's tables as quads (common.h): nreg x 256 dwords, dword (t*16+m) of quad R holds entry (t, m)
+// of table 4R+j in byte j (slot_off); the kernels replicate each dword over the 32 banks. Unused slots
+// of the last quad are 0.
 void append_pass(std::vector<uint32_t>& img, const std::vector<Table>& tbs, int nreg) {
   for (int R = 0; R < nreg; ++R)
     for (int r = 0; r < 256; ++r) {
@@ -386,7 +387,7 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
 
 // LDS bytes of a fast CN / VN launch: table regions, column images, the 2 work counters
 size_t fast_lds(int nt, int ncs) {
-  return (size_t)regions_of(nt) * kRegion + (size_t)ncs * kColImg + 64 + kColPermSlack;
+  return lds_of_quads(regions_of(nt)) + (size_t)ncs * kColImg + 64;
 }
 
 // One pass's column images (colf): per image slot, 16 columns m x {entries t = 0..7, t = 8..15} as nibbles
@@ -491,7 +492,7 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     cn_nt += (int)cdeg.size();
     for (int d : vdeg) vn_nt += (d >= 2);
   }
-  const int max_nt = (kLdsBytes / kRegion) * 4;
+  const int max_nt = (kLdsBytes / kSuper) * 8;   // whole super-regions of 2 quads: 16 tables
   // table slot of each column-fetched input (cn_ncols / vn_ncols): raw fold table, or the degree's
   // final (matching-composed) table; slots are numbered as in the pass images below
   std::vector<int> ccol_slot, vcol_slot;   // column image index -> table slot
@@ -609,9 +610,9 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       HIPCHK(ib_small_private_bytes(CM, VM, &priv, &kname));
       const char* sb = getenv("IBL_SMALL_B");
       h->small_b = priv == 0 ? (sb ? std::max(0, atoi(sb)) : kSmallBatchDefault) : 0;
-      h->s_lds_cn = (size_t)h->cn_nt * kRegion;
-      h->s_lds_vn = (size_t)h->vn_nt * kRegion;
-      h->s_lds_dec = (size_t)h->dec_nt * kRegion;
+      h->s_lds_cn = lds_of_quads(h->cn_nt);
+      h->s_lds_vn = lds_of_quads(h->vn_nt);
+      h->s_lds_dec = lds_of_quads(h->dec_nt);
     }
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
@@ -1131,13 +1132,14 @@ int ib_fused_setup(ibl_ib* h) {
   for (int32_t d : g->h_cn_deg) min_dc = std::min(min_dc, d);
   if (min_dc < 2) return IBL_OK;
   const int nreg = std::max(h->cn_nt, std::max(h->vn_nt, h->dec_nt));
-  size_t lds = (size_t)nreg * (kRegion + 1024) + (size_t)g->n_e * 4 + 16;   // tables, raw images, slots
-  if (lds > (size_t)kLdsBytes) return IBL_OK;
-  // two table sets (see TablePrefetch) where they fit beside the slots; IBL_FUSED_DBUF=0 turns them off (A/B)
-  const size_t lds2 = (size_t)nreg * 2 * kRegion + (size_t)g->n_e * 4 + 16;
+  // one table set: tables, raw images, slots; two sets (see TablePrefetch; a single quad's two sets share
+  // one super-region) where they fit beside the slots; IBL_FUSED_DBUF=0 turns them off (A/B)
+  const size_t lds1 = lds_of_quads(nreg) + (size_t)nreg * 1024 + (size_t)g->n_e * 4 + 16;
+  const size_t lds2 = lds_of_quads(2 * nreg) + (size_t)g->n_e * 4 + 16;
   const char* dbe = getenv("IBL_FUSED_DBUF");
-  const bool dbuf = lds2 <= (size_t)kLdsBytes && !(dbe && dbe[0] == '0');
-  if (dbuf) lds = lds2;
+  const bool dbuf = nreg <= 2 && lds2 <= (size_t)kLdsBytes && !(dbe && dbe[0] == '0');   // set offset: ib_fused
+  const size_t lds = dbuf ? lds2 : lds1;
+  if (lds > (size_t)kLdsBytes) return IBL_OK;
   int bpc = 0, block = 0;
   size_t priv = 0;
   if (ib_fused_occupancy(h->CM, h->VM, 8, lds, &bpc, &block, &priv) != hipSuccess || bpc < 1 || priv != 0) {

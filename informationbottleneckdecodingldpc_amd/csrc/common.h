@@ -31,20 +31,21 @@ constexpr int kChunkIB = 512 * kW;  // codewords per fast-path wave item
 constexpr int kRowPad = 512 * (IBL_LIGHT_W > IBL_W ? IBL_LIGHT_W : IBL_W);   // row padding (codewords)
 constexpr int kChunkDec = 512;      // codewords per decision-kernel wave item
 constexpr int kTbl = 8192;        // LDS bytes per IB lookup table (replicated over the 32 banks)
-// LDS table layout: 4 tables interleaved per 32-KiB region — byte (slot & 3) of the dword at row
-// t*16+m, bank lane&31 holds entry (t, m) of table `slot`, so a lookup address is
-// (t << 11) | (m << 7) | 4*(lane&31) + slot_off(slot) with the slot in the DS immediate.
-constexpr int kRegion = 4 * kTbl;
-// IBL_COLPERM (timing A/B only, wrong results; tools/variants.py colperm): column terms as one
-// v_perm_b32 from nibble-spread words (column stride 256 B, row stride 4 KiB) without the 64-KiB table
-// layout it needs: the lookups read the current layout at those addresses (same banks, so the same LDS
-// cycles); the per-pass launches get one spare region so every address stays inside the allocation.
-#ifndef IBL_COLPERM
-#define IBL_COLPERM 0
-#endif
-constexpr int kColPermSlack = IBL_COLPERM ? kRegion : 0;
-__host__ __device__ constexpr uint32_t slot_off(int s) { return (uint32_t)(s >> 2) * kRegion + (uint32_t)(s & 3); }
-constexpr int regions_of(int nt) { return (nt + 3) >> 2; }
+// LDS table layout (round 5): tables in quads of 4 — byte (slot & 3) of a dword holds table `slot` —
+// and two quads per 64-KiB super-region, interleaved at 128 B: quad q lives in super-region q >> 1,
+// half q & 1 (address bit 7). Entry (t, m) of a table sits at row t (4 KiB stride), column m (256 B),
+// replicated for the 32 banks (lane & 31), so a lookup address is
+//   (t << 12) | (m << 8) | 4*(lane&31) + slot_off(slot)
+// with the slot in the DS immediate for slots < 8. Byte 1 of an address is the column alone, so a
+// column term is one v_perm_b32 that drops a codeword's nibble (spread to a byte) into byte 1 of the
+// lane term (colq); bytes 0, 2, 3 keep the lane, half and super-region bits.
+constexpr int kSuper = 65536;                 // bytes per super-region (2 quads)
+constexpr int kRowSh = 12, kColSh = 8;        // row / column shifts of a lookup address
+__host__ __device__ constexpr uint32_t quad_off(int q) { return (uint32_t)(q >> 1) * kSuper + (uint32_t)(q & 1) * 128u; }
+__host__ __device__ constexpr uint32_t slot_off(int s) { return quad_off(s >> 2) + (uint32_t)(s & 3); }
+constexpr int regions_of(int nt) { return (nt + 3) >> 2; }   // quads of nt tables
+// LDS bytes of nq quads from address 0 (an odd count leaves the last super-region's half 1 unused)
+__host__ __device__ constexpr size_t lds_of_quads(int nq) { return (size_t)((nq + 1) >> 1) * kSuper; }
 // Column images (tools/gen_sched.py "Column fetches"): the last cn_ncols(D) / vn_ncols(D) inputs of a
 // node read their shared table's whole column (16 nibbles, ds_read_b64) instead of one entry per
 // chain. 4 KiB of LDS per table image (16 columns x 32 lane copies x 8 B).

@@ -40,14 +40,12 @@ __device__ __forceinline__ uint32_t lu(uint32_t x, uint32_t c) {
   return *(lds8_t*)(size_t)(x + c);
 }
 // chained lookup: table value t of the previous step, column term q. The row/column merge is one
-// v_lshl_or_b32 per lookup written out, so the compiler cannot hoist t << 11 into a shared
+// v_lshl_or_b32 per lookup written out, so the compiler cannot hoist t << 12 into a shared
 // shift + separate ORs (3 ops for the 2 lookups that read each prefix value P_w).
 __device__ __forceinline__ uint32_t luc(uint32_t t, uint32_t q, uint32_t c) {
   uint32_t x;
-  if constexpr (IBL_COLPERM)
-    asm("v_lshl_or_b32 %0, %1, 12, %2" : "=v"(x) : "v"(t), "v"(q));
-  else
-    asm("v_lshl_or_b32 %0, %1, 11, %2" : "=v"(x) : "v"(t), "v"(q));
+  static_assert(kRowSh == 12, "luc's shift is the row shift of the table layout");
+  asm("v_lshl_or_b32 %0, %1, 12, %2" : "=v"(x) : "v"(t), "v"(q));
   return *(lds8_t*)(size_t)(x + c);
 }
 // Column fetch (tools/gen_sched.py, "Column fetches"): column T(., m) of one table as 16 nibbles
@@ -72,8 +70,9 @@ __device__ __forceinline__ void lds_at_zero(const uint8_t* lds) {
   if (lds_base(lds) != 0u) __builtin_trap();  // uniform scalar test; never taken without static LDS
 }
 
-// column term of a lookup: (m << 7) | 4*(lane & 31); the row term of t is t << 11 (see kRegion)
-__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) { return (m << 7) | lane4; }
+// column term of a lookup: (m << 8) | 4*(lane & 31) (+ half / super-region bits); the row term of t is
+// t << 12 (common.h, table layout)
+__device__ __forceinline__ uint32_t qidx(uint32_t m, uint32_t lane4) { return (m << kColSh) | lane4; }
 
 __device__ __forceinline__ uint32_t valid_mask4(int remaining) {
   return remaining >= 4 ? 0xFu : (remaining <= 0 ? 0u : ((1u << remaining) - 1u));
@@ -84,30 +83,28 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
   return __ballot(gate[lane] != 0) != 0ull;
 }
 
-// img: nreg regions x 256 dwords (row t*16+m, byte j = table 4R+j); replicated over the 32 banks
-// (LDS dword i = img[i >> 5]). Written as 16-byte units (unit u = dwords 4u..4u+3 = img[u >> 3]) by
-// consecutive lanes — conflict-free ds_write_b128 — four units per thread and round with their loads
-// issued together: a quarter of the store instructions of dword stores and a quarter of the dependent
-// load rounds (the 256-thread small-batch kernels staged 3 regions in ~7 us a region with dword stores).
-#ifndef IBL_STAGE_DWORD
-#define IBL_STAGE_DWORD 0   // 1: the round-4 dword-per-thread staging (A/B)
-#endif
+// img: nreg quads x 256 dwords (dword t*16+m of quad q = entry (t, m) of its 4 tables, common.h layout),
+// replicated over the 32 banks. Written as 16-byte units (unit u = LDS bytes 16u..16u+15: super-region
+// u >> 12, row (u >> 8) & 15, column (u >> 4) & 15, half (u >> 3) & 1, lanes 4(u & 7)..+3) by consecutive
+// lanes — conflict-free ds_write_b128 — four units per thread and round with their loads issued together
+// (a quarter of the store instructions and dependent load rounds of dword stores: the 256-thread
+// small-batch kernels staged 3 quads in ~7 us a quad with dword stores). An odd quad count leaves the last
+// super-region's half 1 unwritten (never read).
 __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nreg) {
-  if constexpr (IBL_STAGE_DWORD) {
-    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
-    const int n = nreg * (kRegion / 4);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = img[i >> 5];
-    return;
-  }
   uint4* l4 = reinterpret_cast<uint4*>(lds);
-  const int n = nreg * (kRegion / 16), bd = blockDim.x;
+  const int n = (int)(lds_of_quads(nreg) / 16), bd = blockDim.x;
   for (int u = threadIdx.x; u < n; u += 4 * bd) {
     uint32_t w[4];
+    bool ok[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = u + k * bd < n ? img[(u + k * bd) >> 3] : 0u;
+    for (int k = 0; k < 4; ++k) {
+      const int v = u + k * bd, q = ((v >> 12) << 1) | ((v >> 3) & 1);
+      ok[k] = v < n && q < nreg;
+      w[k] = ok[k] ? img[q * 256 + ((v >> 4) & 255)] : 0u;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (u + k * bd < n) l4[u + k * bd] = make_uint4(w[k], w[k], w[k], w[k]);
+      if (ok[k]) l4[u + k * bd] = make_uint4(w[k], w[k], w[k], w[k]);
   }
 }
 
@@ -123,15 +120,15 @@ __device__ __forceinline__ void stage_cols(uint8_t* dst, const uint32_t* cimg, i
 // codeword c in nibble (c & 1) of byte c/2. A lane owns 8*W consecutive codewords = W dwords of
 // each row (W = rowW<MAXD>()), a wave item = one node x 512*W codewords (256*W-B row segments).
 __device__ __forceinline__ uint32_t nib(uint32_t w, int k) { return __builtin_amdgcn_ubfe(w, 4 * k, 4); }
-// column term of codeword k of input word w (the generated schedules' form). IBL_COLPERM: one v_perm_b32
-// per codeword from the word's even / odd nibbles spread to bytes (w & 0x0F0F0F0F, (w >> 4) & 0x0F0F0F0F,
-// shared by the codewords of a group): byte 0 and bytes 2-3 from the lane term, byte 1 = the nibble.
+// column term of codeword k of input word w (the generated schedules' form): one v_perm_b32 per codeword
+// from the word's even / odd nibbles spread to bytes (w & 0x0F0F0F0F, (w >> 4) & 0x0F0F0F0F, shared by the
+// codewords of a group) — bytes 0, 2, 3 from the lane term, byte 1 = the nibble — instead of a v_bfe and a
+// v_lshl_or. A/B on one box against the round-4 layout's two ops (profiles/r05_colperm_ab.json):
+// C4 176.6k -> 181.0k cw/s, C2 1.791M -> 1.879M. The lane term's byte 1 must be 0 (common.h layout).
 __device__ __forceinline__ uint32_t colq(uint32_t w, int k, uint32_t lane4) {
-  if constexpr (IBL_COLPERM) {
-    const uint32_t src = (k & 1) ? ((w >> 4) & 0x0F0F0F0Fu) : (w & 0x0F0F0F0Fu);
-    return __builtin_amdgcn_perm(src, lane4, 0x03020000u | ((4u + (uint32_t)(k >> 1)) << 8));
-  }
-  return qidx(nib(w, k), lane4);
+  static_assert(kColSh == 8, "colq places the column in byte 1");
+  const uint32_t src = (k & 1) ? ((w >> 4) & 0x0F0F0F0Fu) : (w & 0x0F0F0F0Fu);
+  return __builtin_amdgcn_perm(src, lane4, 0x03020000u | ((4u + (uint32_t)(k >> 1)) << 8));
 }
 
 // all-ones nibbles for the codewords of a word that lie inside the batch
@@ -357,8 +354,8 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
           uint32_t t0[4], t1[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
-            t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
+            t0[s] = lu((nib(in[1], 4 * g + s) << kRowSh) + lane4, fbase);
+            t1[s] = lu((nib(in[0], 4 * g + s) << kRowSh) + lane4, fbase);
           }
           o[0] |= pack4n(t0, g);
           o[1] |= pack4n(t1, g);
@@ -459,7 +456,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int k = 4 * g + s;
-      uint32_t Q = lu((nib(cw, k) << 11) + qidx(nib(inw[0], k), lane4), 0);
+      uint32_t Q = lu((nib(cw, k) << kRowSh) + qidx(nib(inw[0], k), lane4), 0);
 #pragma unroll
       for (int l = 1; l < D; ++l) Q = luc(Q, qidx(nib(inw[l], k), lane4), slot_off(l));
       packed |= Q << (8 * s);
@@ -479,12 +476,12 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 
 // LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
 __device__ __forceinline__ int* lds_counters(const uint8_t* lds, const IbFastArgs& a) {
-  return reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + (size_t)a.nt * kRegion + (size_t)a.ncs * kColImg);
+  return reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + lds_of_quads(a.nt) + (size_t)a.ncs * kColImg);
 }
 __device__ __forceinline__ void stage_pass(uint8_t* lds, const IbFastArgs& a) {
   if (threadIdx.x < 2) lds_counters(lds, a)[threadIdx.x] = 0;
   stage_tables(lds, a.img, a.nt);
-  stage_cols(lds + (size_t)a.nt * kRegion, a.cimg, a.ncs);
+  stage_cols(lds + lds_of_quads(a.nt), a.cimg, a.ncs);
 }
 
 // Persistent wave loop shared by the CN and VN passes: items (position, chunk) are dealt
@@ -614,7 +611,7 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   }
   int* ctr = lds_counters(lds, a);  // 2 phase counters
   // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
-  const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)a.nt * kRegion;
+  const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)lds_of_quads(a.nt);
   // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
   // degree-2/3 variables, few lookups per byte moved) by HBM. The first IBL_MIX quarters of the
   // block's waves take the light share first, so both kinds run side by side on every CU; a wave that
@@ -741,8 +738,8 @@ __device__ __forceinline__ void cn_small_item(const IbFastArgs& a, uint32_t lane
         uint32_t t0[4], t1[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
-          t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
+          t0[s] = lu((nib(in[1], 4 * g + s) << kRowSh) + lane4, fbase);
+          t1[s] = lu((nib(in[0], 4 * g + s) << kRowSh) + lane4, fbase);
         }
         o[0] |= pack4n(t0, g);
         o[1] |= pack4n(t1, g);
@@ -934,8 +931,8 @@ __device__ __forceinline__ void fused_cn_dword(uint32_t* msg, int first, int cnt
         uint32_t t0[4], t1[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          t0[s] = lu((nib(in[1], 4 * g + s) << 11) + lane4, fbase);
-          t1[s] = lu((nib(in[0], 4 * g + s) << 11) + lane4, fbase);
+          t0[s] = lu((nib(in[1], 4 * g + s) << kRowSh) + lane4, fbase);
+          t1[s] = lu((nib(in[0], 4 * g + s) << kRowSh) + lane4, fbase);
         }
         o[0] |= pack4n(t0, g);
         o[1] |= pack4n(t1, g);
@@ -1021,7 +1018,7 @@ __device__ __forceinline__ void fused_dec_dword(const uint32_t* msg, const VnTas
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int k = 4 * g + s;
-      uint32_t Q = lu((nib(v.chw, k) << 11) + qidx(nib(in[0], k), lane4), 0);
+      uint32_t Q = lu((nib(v.chw, k) << kRowSh) + qidx(nib(in[0], k), lane4), 0);
 #pragma unroll
       for (int l = 1; l < D; ++l) Q = luc(Q, qidx(nib(in[l], k), lane4), slot_off(l));
       packed |= Q << (8 * s);
@@ -1030,18 +1027,18 @@ __device__ __forceinline__ void fused_dec_dword(const uint32_t* msg, const VnTas
   }
 }
 
-// Table staging: a pass's raw image is 256 dwords per region (each entry byte-packed 4 tables deep);
-// the LDS image replicates every dword over the 32 banks (l32[i] = img[i >> 5]). Two modes:
+// Table staging: a pass's raw image is 256 dwords per quad (each entry byte-packed 4 tables deep);
+// the LDS image replicates every dword over the 32 banks (common.h layout). Two modes:
 // * single set (dbuf = 0): the next phase's raw dwords are loaded into registers at the START of the
 //   current phase (2 per thread), written to a small raw buffer in LDS when the wave's tasks are done
 //   and replicated LDS -> LDS after the phase barrier (a second barrier follows): the phase boundary
 //   pays LDS traffic only, not an L2 round trip;
-// * two sets (dbuf = 1, when 2 x nreg regions fit beside the slots, e.g. regular (3,6) N=8000): phase p
+// * two sets (dbuf = 1, when 2 x nreg quads fit beside the slots, e.g. regular (3,6) N=8000): phase p
 //   looks up in set p & 1. A thread loads one source dword per 8 replicated dwords of the next phase's
 //   image at the start of the current phase and writes them (two 16-byte stores of the same value) into
 //   the other set when its wave's tasks are done, i.e. while slower waves still compute: one barrier per
 //   phase and no serial replication step. The set is selected through the lookups' column term (lane4
-//   | set offset: the row/column part of an address stays below kRegion, so no extra VALU per lookup).
+//   | set offset: bit 7 for one quad a set, bit 16 for two; no extra VALU per lookup).
 constexpr int kPfSrc = 2;
 struct TablePrefetch {
   uint32_t r[kPfSrc];
@@ -1067,30 +1064,34 @@ struct TablePrefetch {
     }
     for (int i = threadIdx.x + kPfSrc * blockDim.x; i < nsrc; i += blockDim.x) raw[i] = img[i];
   }
-  // single set, after the phase barrier: replicate into the table regions at LDS address 0
+  // single set, after the phase barrier: replicate into the table quads at LDS address 0
   __device__ __forceinline__ void replicate(uint8_t* lds, const uint32_t* raw) const {
-    uint32_t* l32 = reinterpret_cast<uint32_t*>(lds);
-    const int n = nsrc * 32;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) l32[i] = raw[i >> 5];
+    stage_tables(lds, raw, nsrc >> 8);
   }
-  // two sets, before the phase barrier: this thread's units straight into the next phase's set
-  __device__ __forceinline__ void put_set(uint8_t* set) const {
-    uint4* s4 = reinterpret_cast<uint4*>(set);
+  // two sets, before the phase barrier: this thread's units straight into the next phase's set, whose
+  // quads start at quad fq (unit i = 8 of the 32 bank copies of raw dword i >> 2, common.h layout)
+  __device__ __forceinline__ static uint4* unit_at(uint8_t* lds, int fq, int i) {
+    const int rr = i >> 2;
+    return reinterpret_cast<uint4*>(lds + quad_off(fq + (rr >> 8)) + (uint32_t)(rr & 255) * 256u) + 2 * (i & 3);
+  }
+  __device__ __forceinline__ void put_set(uint8_t* lds, int fq) const {
     const int n = nsrc * 4;
 #pragma unroll
     for (int k = 0; k < kPfSrc; ++k) {
       const int i = threadIdx.x + k * blockDim.x;
       if (i < n) {
         const uint4 v = make_uint4(r[k], r[k], r[k], r[k]);
-        s4[2 * i] = v;
-        s4[2 * i + 1] = v;
+        uint4* d = unit_at(lds, fq, i);
+        d[0] = v;
+        d[1] = v;
       }
     }
     for (int i = threadIdx.x + kPfSrc * blockDim.x; i < n; i += blockDim.x) {
       const uint32_t w = img[i >> 2];
       const uint4 v = make_uint4(w, w, w, w);
-      s4[2 * i] = v;
-      s4[2 * i + 1] = v;
+      uint4* d = unit_at(lds, fq, i);
+      d[0] = v;
+      d[1] = v;
     }
   }
 };
@@ -1109,11 +1110,13 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   constexpr int MAXD = VMAX;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   lds_at_zero(lds);
-  // LDS: [nreg table regions][raw images, nreg x 1 KiB][E message slots][2 counters], or with two
-  // table sets (dbuf): [set 0: nreg regions][set 1: nreg regions][E message slots][2 counters]
-  const uint32_t set_off = a.dbuf ? (uint32_t)a.nreg * kRegion : 0u;
-  uint32_t* raw = reinterpret_cast<uint32_t*>(lds + (size_t)a.nreg * kRegion);
-  uint32_t* msg = a.dbuf ? reinterpret_cast<uint32_t*>(lds + 2 * (size_t)set_off) : raw + (size_t)a.nreg * 256;
+  // LDS: [nreg table quads][raw images, nreg x 1 KiB][E message slots][2 counters], or with two
+  // table sets (dbuf): [set 0: nreg quads][set 1: nreg quads][E message slots][2 counters]
+  // (set 1 = quads nreg..2 nreg-1: at + 128 B for one quad a set, + 64 KiB for two — an offset that adds to
+  // every slot's, so it rides in the lanes' column term; the host allows two sets only for nreg <= 2)
+  const uint32_t set_off = a.dbuf ? quad_off(a.nreg) : 0u;
+  uint32_t* raw = reinterpret_cast<uint32_t*>(lds + lds_of_quads(a.nreg));
+  uint32_t* msg = a.dbuf ? reinterpret_cast<uint32_t*>(lds + lds_of_quads(2 * a.nreg)) : raw + (size_t)a.nreg * 256;
   int* ctr = reinterpret_cast<int*>(msg + a.n_e);
   const int lane = threadIdx.x & 63;
   const uint32_t lane4c = (uint32_t)(lane & 31) << 2;
@@ -1140,7 +1143,7 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   };
   auto next_phase = [&]() __attribute__((always_inline)) {
     if (pf.dbuf) {
-      pf.put_set(lds + (((ph + 1) & 1) ? set_off : 0u));
+      pf.put_set(lds, ((ph + 1) & 1) ? a.nreg : 0);
       __syncthreads();
       mark(3 * ph + 1);   // all waves done with the phase (and the next phase's set written)
       mark(3 * ph + 2);

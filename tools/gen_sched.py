@@ -38,8 +38,8 @@ import sys
 KMAXD = 16
 
 
-def slot_off(l):
-    return (l >> 2) * 32768 + (l & 3)
+def slot_off(l):   # csrc/common.h: quad l >> 2 in super-region l >> 3, half (l >> 2) & 1, byte l & 3
+    return (l >> 3) * 65536 + ((l >> 2) & 1) * 128 + (l & 3)
 
 
 def cn_ncols(D, nc):

@@ -57,16 +57,12 @@ VARIANTS = {
     "ntcn": ["IBL_NT_CN=1"],
     # float variable items over 2-KiB row segments (two 16-byte pieces per lane)
     "flvn2": ["IBL_FL_VN2=1"],
-    # round-4 table staging (one dword store per thread and round) for the A/B of the 16-byte staging
-    "stagedw": ["IBL_STAGE_DWORD=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
     "ieeeon": [],
     # min-sum check node with the (min, second min) pair for every degree (the round-3 form)
     "msps0": ["IBL_MS_PS=0"],
     # fused float check tasks without the constant-stride body for full tasks
     "cn64off": ["IBL_FL_CN64=0"],
-    # timing A/B (wrong results): v_perm_b32 column terms at their real instruction cost (common.h IBL_COLPERM)
-    "colperm": ["IBL_COLPERM=1"],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
