@@ -297,20 +297,12 @@ __device__ __forceinline__ uint32_t pack4n(const uint32_t (&t)[4], int g) {
 #endif
 #include IBL_SCHED_FILE
 
-#ifndef IBL_WORD_UNROLL
-#define IBL_WORD_UNROLL 0   // A/B (tools/variants.py wu1 / wu3): bit 0 check words, bit 1 variable words unrolled
-#endif
 // NCW: codewords of the word that are computed (nibbles 0 .. NCW-1; 4 = the fused kernel's half groups)
 template <int D, int NCW = 8>
 __device__ __forceinline__ void cn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t fbase,
                                         const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
-  if constexpr (IBL_WORD_UNROLL & 1) {   // A/B: groups unrolled (the spread words shared by a word's groups)
-#pragma unroll
-    for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
-  } else {
-#pragma unroll 1
-    for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
-  }
+#pragma unroll 1   // unrolled (the spread words shared by a word's groups) the check body spills: 56 B at MAXD=8
+  for (int k0 = 0; k0 < NCW; k0 += cn_sched_s(D)) cn_group<D>(lane4, in, fbase, cb, outw, k0);
 }
 
 // column-image addresses of the column-fetched inputs of a degree-D node (cb of colf)
@@ -390,13 +382,8 @@ __device__ __forceinline__ void cn_compute(const IbFastArgs& a, uint32_t lane4, 
 template <int D, int NCW = 8>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
-  if constexpr (IBL_WORD_UNROLL & 2) {
-#pragma unroll
-    for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
-  } else {
 #pragma unroll 1
-    for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
-  }
+  for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
 
 template <int D, class Buf>

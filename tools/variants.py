@@ -63,9 +63,6 @@ VARIANTS = {
     "msps0": ["IBL_MS_PS=0"],
     # fused float check tasks without the constant-stride body for full tasks
     "cn64off": ["IBL_FL_CN64=0"],
-    # per-pass check / variable words with their codeword groups unrolled (A/B)
-    "wu1": ["IBL_WORD_UNROLL=1"],
-    "wu3": ["IBL_WORD_UNROLL=3"],
 }
 # per-source flag overrides (replace _build.SRC_FLAGS)
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
