@@ -88,7 +88,7 @@ int ibl_ib_path(const ibl_ib* h);
 /*
  * Decode path of an IB decoder on the fast path (no reference counterpart; results are identical):
  *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits (E * 4 bytes of messages
- *                            for 8 codewords plus the largest pass's table regions <= 160 KiB,
+ *                            for 8 codewords plus the largest pass's table quads <= 160 KiB,
  *                            check degrees >= 2; e.g. regular (3,6) N=8000, WLAN), else per-pass;
  *   IBL_PATH_PASSES          one launch per check / variable pass, messages in HBM;
  *   IBL_PATH_FUSED           the fused kernel (IBL_EUNSUPPORTED if the code does not fit).

@@ -93,7 +93,7 @@ struct IbFastArgs {
   const int32_t* gate;      // kShards flag words that must be non-zero to run (nullptr: run)
   int32_t* unsat;           // kShards flag words to set when a check is unsatisfied (nullptr: no syndrome)
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
-  int32_t nt;               // 32-KiB table regions staged in LDS (4 tables each)
+  int32_t nt;               // table quads staged in LDS (4 tables each, common.h layout)
   const uint32_t* cimg;     // this pass's column images: ncs x 16 columns x 2 dwords (stage_cols)
   int32_t ncs;              // column images staged after the table regions
   int8_t ccol[kMaxD + 1][4];// per degree: column image of its i-th column-fetched input
@@ -138,7 +138,7 @@ struct IbFusedArgs {
   int32_t* unsat;           // non-null: CN pass j >= 1 ORs "unsatisfied" into unsat[j*kShards + shard]
   const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
   int32_t cn_fslot[kMaxD + 1], vn_fslot[kMaxD + 1];
-  int32_t cn_nt, vn_nt, dec_nt, nreg;   // regions per pass image; nreg = table regions reserved in LDS
+  int32_t cn_nt, vn_nt, dec_nt, nreg;   // quads per pass image; nreg = table quads reserved in LDS (per set)
   int32_t dbuf;             // 1: two table sets of nreg regions (phase p reads set p & 1; the next phase's
                             // set is written during the current phase), no raw buffer
   int32_t n_cn_nodes;
