@@ -40,6 +40,9 @@ VARIANTS = {
     "w1s8": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1s8.inc"'],
     "w1l4": ["IBL_W=1", 'IBL_SCHED_FILE="ib_sched_w1l4.inc"'],
     "w2l4": ['IBL_SCHED_FILE="ib_sched_w2l4.inc"'],
+    "cl3": ['IBL_SCHED_FILE="ib_sched_cl3.inc"'],
+    "v4l2": ['IBL_SCHED_FILE="ib_sched_v4l2.inc"'],
+    "v2l3": ['IBL_SCHED_FILE="ib_sched_v2l3.inc"'],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1"],
     # timing-only host hooks (IBL_VN_PART, IBL_TRACE_WAVES, IBL_DEBUG_SYNC): not in the product build
@@ -68,7 +71,7 @@ VARIANTS = {
 SRC_FLAGS = {"ieeeon": {"float_kernels.hip": ["-fno-honor-nans"]}}
 # gen_sched.py arguments of the variants that need their own schedule file
 SCHED_ARGS = {"nc23": "4 2 2 4 2 3", "nc22": "4 2 2 4 2 2", "nc33": "4 2 2 4 3 3", "s2": "2 4 2 4 2 3",
-              "s2n": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0"}
+              "s2n": "2 4 2 4 0 0", "w1s8": "8 2 2 4 0 0", "w1l4": "4 4 2 4 0 0", "w2l4": "4 4 2 4 0 0", "cl3": "4 3 2 4 0 0", "v4l2": "4 2 4 2 0 0", "v2l3": "4 2 2 3 0 0"}
 
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
