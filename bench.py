@@ -150,8 +150,7 @@ def _pmc_traffic(path, kind, kname, B, fmt):
     return None
 
 
-def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec, folded=0,
-             persist_passes=None):
+def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec, folded=0):
     """Roofline of the dominant kernel, priced at the bytes it actually moves.
 
     Per-pass kernels (HBM-bound by design): check pass reads E message rows and writes E; variable
@@ -225,20 +224,6 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
                 "note": "fused on-chip decoder: messages of 4 codewords per workgroup stay in LDS for all "
                         "iterations; LDS roofline at this kernel's 16-B read/write mix (MI355X_MICROARCH.md §LDS)",
                 "launches": {"fused": cn_n}}
-    if persist_passes is not None:
-        # persistent small-batch IB loop (ib_small_persist): one launch runs every pass of a decode — the mean
-        # (check, variable) passes per launch — so its bytes are the passes' row bytes at u4; latency-bound at
-        # the batches it serves (B <= 192)
-        ncn, nvn = persist_passes
-        kbytes = int((cn_bytes_u8 * ncn + vn_bytes_u8 * nvn) * ws / w)
-        t = cn_avg * 1e-3
-        ach = kbytes / t / 1e9 if t > 0 else 0.0
-        return {"bound": "hbm", "kernel": "ib_small_persist", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None, "bytes_per_launch": kbytes,
-                "format": fmt, "avg_launch_ms": round(cn_avg, 4), "launches": {"persistent": cn_n},
-                "passes_per_launch": {"cn": round(ncn, 2), "vn": round(nvn, 2)},
-                "note": "one cooperative launch per decode runs every check / variable pass with grid barriers "
-                        "between them; at B <= 192 it is latency-bound, so frac is far below 1 by construction"}
     if vn_ms >= cn_ms:
         kname = "ib_vn_fast" if fmt == "u4" else ("ib_vn_gen" if a.kind == "ib" else "fl_vn")
         kavg, ku8 = vn_avg, vn_bytes_u8
@@ -270,7 +255,7 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
         lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
         avg = {"cn": cn_avg, "vn": vn_avg}
         roof["lds_lookups_per_clk_per_cu"] = {k: round(lk[k] / (avg[k] * 1e-3) / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2)
-                                              for k in lk if avg[k] > 0}
+                                              for k in lk}
         roof["lds_lookups_per_clk_per_cu"]["ceiling"] = 32.0
         mc = measured_lookup_ceiling()
         if mc:
@@ -600,11 +585,8 @@ def main():
     fmt = "u4" if fast else ("u8" if a.kind == "ib" else "f32")
     if a.kind == "ib":
         dtype = fmt
-    persist = small and a.kind == "ib" and getattr(dec, "small_persistent", False)
-    # passes one persistent launch runs: check passes 0..L, variable passes 0..L-1 (L = the stop iteration)
-    pp = (float(stop_it.mean()) + 1, float(stop_it.mean())) if persist else None
     roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec,
-                    folded=folded, persist_passes=pp)
+                    folded=folded)
     # HBM bytes the decode moves per codeword at the stored widths (channel in, output out: u8 for IB, fp32 float)
     moved = moved_bytes_per_cw(g.n_e, n_v, I, "fused" if fused else "passes", ws, w, w, w_stage=w, folded=folded)
     cpu = None
@@ -635,7 +617,7 @@ def main():
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, "
                                    f"{('matching ' + ('on' if match else 'off') + ', ') if a.kind == 'ib' else ''}"
-                                   f"{'fused on-chip kernel' if fused else (('small-batch persistent kernel' if persist else 'small-batch per-pass kernels') if small else 'per-pass kernels')}"
+                                   f"{'fused on-chip kernel' if fused else ('small-batch per-pass kernels' if small else 'per-pass kernels')}"
                                    f"{', early stop on (batch-global)' if early else ', fixed iterations'}",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "early_stop": early, "ebn0_db": a.ebn0, "batch_offset": a.batch_offset,

@@ -163,14 +163,3 @@ def test_bench_arguments(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "C1", "--ebn0", "2.5"])
     a = bench.parse()
     assert a.no_match and a.ebn0 == 2.5 and a.batch_per_gpu == 1000
-
-
-def test_persistent_small_batch_roofline(dvb):
-    """A persistent small-batch launch (ib_small_persist) runs every pass of a decode: its bytes are the
-    check passes' 2E rows and the variable passes' 2E + N rows at u4 for the passes it ran."""
-    g, B = dvb, 2
-    r = bench.roofline(_args(), g, g.n_v, B, 50, 1, 0.5, "u4", True, False, cn_avg=0.8, vn_avg=0.0,
-                       cn_ms=8.0, vn_ms=0.0, cn_n=10, vn_n=0, dec=None, persist_passes=(20.0, 19.0))
-    assert r["kernel"] == "ib_small_persist" and r["launches"] == {"persistent": 10}
-    assert r["bytes_per_launch"] == int((2 * g.n_e * B * 20 + (2 * g.n_e + g.n_v) * B * 19) * 0.5)
-    assert 0 < r["frac"] < 0.05
