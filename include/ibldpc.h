@@ -109,15 +109,6 @@ int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
 int ibl_ib_set_small_batch(ibl_ib* h, int32_t max_b);
 int ibl_ib_small_batch(const ibl_ib* h, int32_t* max_b);
 /*
- * *on = 1 when the small-batch decode loop runs as ONE persistent cooperative launch (one workgroup per CU,
- * grid barriers between the passes, the early stop taken inside the launch) instead of one launch per
- * pass; same outputs and stop iteration (no reference counterpart).  On by default where the cooperative
- * launch fits; IBL_SMALL_PERSIST=0 in the environment when the decoder is created keeps the per-pass small
- * kernels.  A grid barrier that times out (only possible if the workgroups were not co-resident) makes the
- * decode report -1 iterations through d_iters.
- */
-int ibl_ib_small_persistent(const ibl_ib* h, int32_t* on);
-/*
  * Codewords per workgroup the fused kernel runs a batch of B with (no reference counterpart; results are
  * identical either way): 8, or 4 (half groups) when 2 * ceil(B / 8) workgroups fit the grid or the
  * environment IBL_FUSED_NCW=4 forces them and the half-group kernel fits the device; 0 when decodes do

@@ -27,7 +27,7 @@ EXPORTS = [
     "ibl_version", "ibl_last_error", "ibl_device_count", "ibl_map_node_connections",
     "ibl_graph_create", "ibl_graph_info", "ibl_graph_destroy",
     "ibl_ib_create", "ibl_ib_path", "ibl_ib_set_path", "ibl_ib_path_in_use", "ibl_ib_fused_ncw", "ibl_ib_decode",
-    "ibl_ib_set_small_batch", "ibl_ib_small_batch", "ibl_ib_small_persistent",
+    "ibl_ib_set_small_batch", "ibl_ib_small_batch",
     "ibl_ib_destroy",
     "ibl_float_create", "ibl_float_decode", "ibl_float_destroy", "ibl_count_below",
     "ibl_float_set_path", "ibl_float_path_in_use", "ibl_float_folded", "ibl_float_input_check",
@@ -79,7 +79,6 @@ def load():
     L.ibl_ib_fused_ncw.argtypes = [_vp, _i32, ctypes.POINTER(_i32)]
     L.ibl_ib_set_small_batch.argtypes = [_vp, _i32]
     L.ibl_ib_small_batch.argtypes = [_vp, ctypes.POINTER(_i32)]
-    L.ibl_ib_small_persistent.argtypes = [_vp, ctypes.POINTER(_i32)]
     L.ibl_ib_decode.argtypes = [_vp, _vp, _i32, _i32, _vp, _i32, _i32, _vp, _vp]
     L.ibl_ib_destroy.argtypes = [_vp]
     L.ibl_ib_destroy.restype = None

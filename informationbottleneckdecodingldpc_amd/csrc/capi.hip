@@ -197,10 +197,6 @@ struct ibl_ib {
   // small-batch per-pass kernels (ib_*_small) for B <= small_b (0: off); LDS bytes per launch kind
   int32_t small_b = 0;
   size_t s_lds_cn = 0, s_lds_vn = 0, s_lds_dec = 0;
-  // persistent small-batch decode loop (ib_small_persist): on / grid / LDS bytes, and its [barrier, error] words
-  int32_t s_persist = 0, s_pgrid = 0;
-  size_t s_plds = 0;
-  int32_t* s_bar = nullptr;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
@@ -617,25 +613,6 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       h->s_lds_cn = lds_of_quads(h->cn_nt);
       h->s_lds_vn = lds_of_quads(h->vn_nt);
       h->s_lds_dec = lds_of_quads(h->dec_nt);
-      // the small-batch loop as one persistent cooperative launch where one workgroup per CU fits
-      // (IBL_SMALL_PERSIST=0 at create keeps the per-pass small kernels: A/B, tests)
-      const char* sp = getenv("IBL_SMALL_PERSIST");
-      int coop = 0;
-      if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, g->device) != hipSuccess) coop = 0;
-      if (h->small_b > 0 && coop && !(sp && sp[0] == '0') && h->cn_nt * 256 <= kSmallBlock &&
-          h->vn_nt * 256 <= kSmallBlock) {
-        const size_t plds = std::max(h->s_lds_cn, h->s_lds_vn);
-        int bpc = 0;
-        size_t pp = 0;
-        if (ib_small_persist_occupancy(std::max(CM, VM), plds, &bpc, &pp) == hipSuccess && bpc >= 1 && pp == 0) {
-          if ((rc = dalloc(&h->s_bar, 2))) return bail(rc);
-          h->s_persist = 1;
-          h->s_pgrid = bpc * g->num_cus;
-          h->s_plds = plds;
-        } else {
-          (void)hipGetLastError();
-        }
-      }
     }
   } else {
     h->cn_len = cn_len; h->vn_len = vn_len;
@@ -663,12 +640,6 @@ int ibl_ib_set_small_batch(ibl_ib* h, int32_t max_b) {
 int ibl_ib_small_batch(const ibl_ib* h, int32_t* max_b) {
   if (!h || !max_b) return fail(IBL_EINVAL, "NULL argument");
   *max_b = h->small_b;
-  return IBL_OK;
-}
-
-int ibl_ib_small_persistent(const ibl_ib* h, int32_t* on) {
-  if (!h || !on) return fail(IBL_EINVAL, "NULL argument");
-  *on = h->s_persist;
   return IBL_OK;
 }
 
@@ -722,7 +693,7 @@ void ibl_ib_destroy(ibl_ib* h) {
   dfree(h->cin); dfree(h->vin); dfree(h->ch8); dfree(h->flags); dfree(h->dL);
   dfree(h->cn_img); dfree(h->vn_img); dfree(h->dec_img); dfree(h->cn_cimg); dfree(h->vn_cimg);
   dfree(h->cn_lut); dfree(h->vn_lut); dfree(h->mc); dfree(h->mv);
-  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot); dfree(h->s_bar);
+  dfree(h->f_cn_task); dfree(h->f_vn_task); dfree(h->f_vn_node); dfree(h->f_vn_slot);
   delete h;
 }
 
@@ -815,18 +786,6 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     std::memcpy(cn.fslot, h->cn_fslot, sizeof(cn.fslot));
     std::memcpy(vn.fslot, h->vn_fslot, sizeof(vn.fslot));
     const int gcn = grid_of(g->n_cn_task, h->s_lds_cn), gvn = grid_of(g->n_vn_task, h->s_lds_vn);
-    const int32_t* perr = nullptr;
-    if (h->s_persist) {   // the whole loop in one cooperative launch (ib_small_persist)
-      IbPersistArgs p{};
-      p.cn = cn; p.vn = vn;
-      p.cn.in = h->cin; p.cn.gather = g->csr_cols; p.cn.img = h->cn_img;
-      p.vn.img = h->vn_img;
-      p.flags = h->flags; p.bar = h->s_bar; p.err = h->s_bar + 1;
-      p.I = I; p.early = early ? 1 : 0;
-      HIPCHK(hipMemsetAsync(h->s_bar, 0, 2 * sizeof(int32_t), s));
-      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_small_persist(p, std::max(h->CM, h->VM), h->s_pgrid, h->s_plds, s); }));
-      perr = h->s_bar + 1;
-    } else {
     cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
     HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
     cn.gather = nullptr;
@@ -841,8 +800,7 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
       cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
       HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
     }
-    }
-    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s, perr));
+    HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     IbDecArgs dc{};
     dc.vin = h->vin; dc.ch8 = h->ch8; dc.img = h->dec_img; dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype;
     dc.nt = h->dec_nt; dc.n_nodes = g->n_v; dc.ldb = ldbb; dc.B = B;

@@ -280,18 +280,7 @@ hipError_t ib_fused_occupancy(int cmax, int vmax, int ncw, size_t lds, int* bloc
 hipError_t launch_ib_cn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_vn_gen(const IbGenArgs& a, hipStream_t s);
 hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);
-hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s,
-                           const int32_t* err = nullptr);
-// persistent small-batch IB decode loop (ib_small_persist): check pass 0 .. the stop, one cooperative launch
-struct IbPersistArgs {
-  IbFastArgs cn, vn;        // as for ib_cn_small / ib_vn_small; cn.in = check inbox and cn.gather = csr_cols (pass 0)
-  int32_t* flags;           // imax x kShards syndrome flags (zeroed by the caller when early)
-  int32_t* bar;             // grid-barrier counter, zeroed by the caller
-  int32_t* err;             // barrier timeout flag, zeroed by the caller
-  int32_t I, early;         // passes: check pass 0, then I-1 x {variable, check}
-};
-hipError_t launch_ib_small_persist(const IbPersistArgs& p, int maxd, int grid, size_t lds, hipStream_t s);
-hipError_t ib_small_persist_occupancy(int maxd, size_t lds, int* blocks_per_cu, size_t* private_bytes);
+hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s);
 // ------------------------------------------------------------ channel generation
 constexpr int kMaxT = 64;         // largest channel alphabet of ibl_channel_sample
 struct ChArgs {

@@ -22,7 +22,6 @@
 //     into the check-node pass (parity of its inputs), and published as device flags that
 //     gate the next launches — no host readback inside the iteration loop.
 #include <algorithm>
-#include <type_traits>
 
 #include "common.h"
 
@@ -863,110 +862,6 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
   });
 }
 
-// ------------------------------------------------------- persistent small-batch decoder
-// The small-batch pass schedule (ib_cn_small / ib_vn_small above, same item bodies and work order) as ONE
-// launch: every pass of the decode loop runs in a grid of one 1024-thread workgroup per CU (all resident:
-// cooperative launch), separated by grid barriers, instead of ~2·i_max launches whose ~3-us gaps and
-// per-launch table staging dominate at B = 2. A pass's raw tables (<= 4 quads = 1024 dwords) are loaded
-// one dword per thread while the previous pass runs and replicated into LDS after the barrier. Early stop:
-// after check pass j every workgroup reads pass j's syndrome flags (the same words finalize_iters reads)
-// and leaves the loop when none is set — the passes the gated launches would have skipped are not run.
-// Grid barrier: each wave's stores complete (s_waitcnt), workgroup barrier, one thread releases at agent
-// scope (L2 write-back), bumps a device counter and spins (agent-scope loads, s_sleep) until every
-// workgroup has arrived, then acquires (L2 / L1 invalidate). The spin is bounded: a workgroup that waits
-// past kBarSpin rounds sets *err and every later barrier returns at once, so the grid always drains;
-// finalize_iters then reports -1 iterations (a barrier can only time out if the workgroups were not
-// co-resident, which the cooperative launch rules out).
-constexpr int kBarSpin = 1 << 22;   // x s_sleep 2 (~128 clocks): ~0.2 s per barrier
-__device__ __forceinline__ void grid_barrier(int32_t* bar, int32_t& target, int32_t* err) {
-  target += (int32_t)gridDim.x;
-  __builtin_amdgcn_s_waitcnt(0);   // this wave's stores acknowledged by L2
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int k = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++k) {
-      if (k >= kBarSpin) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      if ((k & 255) == 255 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
-// one raw table dword per thread (tid < nraw) into its 32 bank copies (common.h layout)
-__device__ __forceinline__ void put_raw_dword(uint8_t* lds, uint32_t w, int tid, int nraw) {
-  if (tid < nraw) {
-    uint4* d = reinterpret_cast<uint4*>(lds + quad_off(tid >> 8) + (uint32_t)(tid & 255) * 256u);
-    const uint4 v = make_uint4(w, w, w, w);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = v;
-  }
-}
-
-template <int MAXD>
-__global__ __launch_bounds__(kSmallBlock) void ib_small_persist(IbPersistArgs p) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  lds_at_zero(lds);
-  const int lane = threadIdx.x & 63, tid = threadIdx.x;
-  const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
-  const int nrc = p.cn.nt * 256, nrv = p.vn.nt * 256;
-  const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
-  int32_t target = 0;
-  auto cn_pass = [&](auto gather_c, bool do_par, int32_t* unsat_w) __attribute__((always_inline)) {
-    constexpr bool G = decltype(gather_c)::value;
-    bool unsat = false;
-    small_items(p.cn, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-      const int st = p.cn.info[4 * pos + 1];
-      switch (d) {
-#define X(D) case D: if constexpr (D <= MAXD) cn_small_item<D, G>(p.cn, lane4, st, c, do_par, unsat); break;
-        IBL_DEG_CASES(X)
-#undef X
-        default: break;
-      }
-    });
-    if (do_par && __ballot(unsat) != 0ull && lane == 0) atomicOr(&unsat_w[shard], 1);
-  };
-  auto vn_pass = [&]() __attribute__((always_inline)) {
-    small_items(p.vn, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-      const int node = p.vn.info[4 * pos], st = p.vn.info[4 * pos + 1];
-      switch (d) {
-        case 1: vn_small_item<1>(p.vn, lane4, node, st, c); break;
-#define X(D) case D: if constexpr (D <= MAXD) vn_small_item<D>(p.vn, lane4, node, st, c); break;
-        IBL_DEG_CASES(X)
-#undef X
-        default: break;
-      }
-    });
-  };
-  // check pass 0 (channel rows gathered through the CSR columns)
-  uint32_t pre = tid < nrc ? p.cn.img[tid] : 0u;
-  put_raw_dword(lds, pre, tid, nrc);
-  __syncthreads();
-  if (p.I > 1) pre = tid < nrv ? p.vn.img[tid] : 0u;
-  cn_pass(std::integral_constant<bool, true>{}, false, nullptr);
-  grid_barrier(p.bar, target, p.err);
-  for (int j = 1; j < p.I; ++j) {
-    put_raw_dword(lds, pre, tid, nrv);   // variable pass j-1
-    __syncthreads();
-    pre = tid < nrc ? p.cn.img[(size_t)j * nrc + tid] : 0u;
-    vn_pass();
-    grid_barrier(p.bar, target, p.err);
-    put_raw_dword(lds, pre, tid, nrc);   // check pass j (+ syndrome of its inputs)
-    __syncthreads();
-    if (j + 1 < p.I) pre = tid < nrv ? p.vn.img[(size_t)j * nrv + tid] : 0u;
-    int32_t* fl = p.flags + (size_t)j * kShards;
-    cn_pass(std::integral_constant<bool, false>{}, p.early != 0, fl);
-    grid_barrier(p.bar, target, p.err);
-    if (p.early && __ballot(__hip_atomic_load(&fl[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) == 0ull)
-      break;   // batch-global stop after check pass j (uniform: every workgroup reads the same flags)
-  }
-}
-
 // ------------------------------------------------------------- fused on-chip decoder
 // For short codes (E * 4 B of messages plus the largest pass's table regions within the CU's LDS,
 // e.g. regular (3,6) N=8000: 96 KB + 32 KB), one workgroup decodes 8 codewords (a dword of 4-bit
@@ -1598,17 +1493,9 @@ __global__ void ib_dec_gen(IbGenDecArgs a) {
 // --------------------------------------------------- stop iteration + error counter
 // L = first loop iteration j in [1, imax-1] whose flags are all zero (syndrome satisfied),
 // else imax-1: the i_num-1 of decode_OpenCL (discrete_LDPC_decoder_irreg.py:277-333).
-__global__ void finalize_iters(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user,
-                               const int32_t* err) {
+__global__ void finalize_iters(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user) {
   const int lane = threadIdx.x & 63;
   int L = imax - 1;
-  if (err && *err != 0) {   // a persistent decode's grid barrier timed out (ib_small_persist)
-    if (lane == 0) {
-      *dL = L;
-      if (user) *user = -1;
-    }
-    return;
-  }
   if (early) {
     for (int j = 1; j <= imax - 1; ++j) {
       if (__ballot(flags[(size_t)j * kShards + lane] != 0) == 0ull) {
@@ -1815,29 +1702,9 @@ hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(ib_dec_gen, dim3(gen_grid(a.n_nodes, a.B)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
-hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s,
-                           const int32_t* err) {
-  hipLaunchKernelGGL(finalize_iters, dim3(1), dim3(64), 0, s, flags, imax, early, dL, user, err);
+hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_iters, dim3(1), dim3(64), 0, s, flags, imax, early, dL, user);
   return hipGetLastError();
-}
-hipError_t launch_ib_small_persist(const IbPersistArgs& p, int maxd, int grid, size_t lds, hipStream_t s) {
-  if (!ib_small_args_ok(p.cn, false) || !p.cn.gather || !p.cn.in || !ib_small_args_ok(p.vn, true) || !p.bar ||
-      !p.err || !p.flags || p.I < 1 || p.cn.nt * 256 > kSmallBlock || p.vn.nt * 256 > kSmallBlock)
-    return hipErrorInvalidValue;
-  IbPersistArgs q = p;
-  void* args[] = {&q};
-  const void* f = maxd <= 8 ? (const void*)ib_small_persist<8> : (const void*)ib_small_persist<16>;
-  return hipLaunchCooperativeKernel(f, dim3(grid), dim3(kSmallBlock), args, (unsigned)lds, s);
-}
-// workgroups of ib_small_persist per CU at this LDS size (0 if it cannot run), and its private segment
-hipError_t ib_small_persist_occupancy(int maxd, size_t lds, int* blocks_per_cu, size_t* private_bytes) {
-  const void* f = maxd <= 8 ? (const void*)ib_small_persist<8> : (const void*)ib_small_persist<16>;
-  hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-  if (e != hipSuccess) return e;
-  hipFuncAttributes fa;
-  if ((e = hipFuncGetAttributes(&fa, f)) != hipSuccess) return e;
-  *private_bytes = fa.localSizeBytes;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, kSmallBlock, lds);
 }
 hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
                               unsigned long long* cnt, hipStream_t s) {

@@ -124,13 +124,6 @@ class IBDecoder:
     def small_batch(self, max_b: int) -> None:
         _lib.check(_lib.load().ibl_ib_set_small_batch(self._h, int(max_b)), "ibl_ib_set_small_batch")
 
-    @property
-    def small_persistent(self) -> bool:
-        """Whether small batches run as one persistent launch (``ibl_ib_small_persistent``)."""
-        n = ctypes.c_int32()
-        _lib.check(_lib.load().ibl_ib_small_persistent(self._h, ctypes.byref(n)), "ibl_ib_small_persistent")
-        return bool(n.value)
-
     def fused_ncw(self, B: int) -> int:
         """Codewords per workgroup the fused kernel decodes a batch of ``B`` with (8, or 4 for half
         groups; 0 when the fused kernel is not in use) — ``ibl_ib_fused_ncw``."""

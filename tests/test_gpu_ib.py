@@ -60,12 +60,10 @@ def test_decode_ignores_diagnostic_environment(eng, dvb_H, monkeypatch):
     ("dvb", 4, 130, True, False, None),      # 17 words, forced onto the small kernels
     ("mixed16", 6, 9, False, True, None),    # every body of the MAXD=16 instantiations (degrees 2..16 / 1..16)
     ("mixed8", 7, 64, True, True, 4.0)])     # MAXD=8 bodies with matching, converging
-def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H, monkeypatch):
-    """The small-batch kernels (wave item = up to 64 same-degree nodes x 8 codewords) — as one persistent
-    cooperative launch with grid barriers (ib_small_persist, the default where it fits) and as one launch per
-    pass (IBL_SMALL_PERSIST=0) — and the fast kernels (wave item = one node x 1024 codewords) all equal the
-    oracle at small B, with the same stop iteration; u8 and i32 in and out; a decoder sized for a larger
-    max_batch (wider rows) too."""
+def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H):
+    """The small-batch per-pass kernels (ib_*_small: wave item = up to 64 same-degree nodes x 8 codewords) and
+    the fast kernels (wave item = one node x 1024 codewords) both equal the oracle at small B, with the same
+    stop iteration; u8 and i32 in and out; a decoder sized for a larger max_batch (wider rows) too."""
     H = {"dvb": lambda: dvb_H,
          "mixed16": lambda: _mixed_code(np.arange(2, 17), np.arange(1, 17), 600, seed=15),
          "mixed8": lambda: _mixed_code(np.array([3, 5, 6, 7, 8]), np.array([2, 3, 5, 6, 7, 8]), 500, seed=5)}[name]()
@@ -81,17 +79,12 @@ def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H, m
     ref, ref_it = oracle.ib_decode(g, tb, ch, match=match, early_stop=early, return_iters=True)
     if name == "dvb" and ebn0 is not None and early:
         assert ref_it < imax - 1            # the batch-global stop happens inside the loop
-    runs = [("1", 1024, None, torch.int32), ("1", 1024, 5000, torch.uint8), ("0", 1024, None, torch.int32),
-            ("0", 1024, 5000, torch.uint8), ("1", 0, None, torch.int32)]
-    for persist, small_b, mb, dt in runs:
-        monkeypatch.setenv("IBL_SMALL_PERSIST", persist)
+    for small_b, mb, dt in ((1024, None, torch.int32), (1024, 5000, torch.uint8), (0, None, torch.int32)):
         out, it, dec = _run(eng, g, tb, ch, match, early, path="passes", small_b=small_b, max_batch=mb,
                             out_dtype=dt, ch_dtype=dt)
         assert dec.fast_path and not dec.fused and dec.small_batch == small_b
-        if name != "mixed16":   # the MAXD=16 persistent kernel spills (the decoder then keeps one launch per pass)
-            assert dec.small_persistent == (persist == "1")
-        assert it == ref_it, (persist, small_b, mb)
-        np.testing.assert_array_equal(out, ref, err_msg=f"persist={persist} small_b={small_b} max_batch={mb}")
+        assert it == ref_it, (small_b, mb)
+        np.testing.assert_array_equal(out, ref, err_msg=f"small_b={small_b} max_batch={mb}")
 
 
 def test_ib_small_batch_default_and_generic(eng, wlan_H):
