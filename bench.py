@@ -255,7 +255,7 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
         lk = {"cn": int(sum(cn_lk(int(d)) for d in g.cn_deg)) * B, "vn": int(sum(vn_lk(int(d)) for d in g.vn_deg)) * B}
         avg = {"cn": cn_avg, "vn": vn_avg}
         roof["lds_lookups_per_clk_per_cu"] = {k: round(lk[k] / (avg[k] * 1e-3) / (NUM_CUS * LDS_CLK_GHZ * 1e9), 2)
-                                              for k in lk}
+                                              for k in lk if avg[k] > 0}
         roof["lds_lookups_per_clk_per_cu"]["ceiling"] = 32.0
         mc = measured_lookup_ceiling()
         if mc:
