@@ -84,27 +84,57 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
 }
 
 // img: nreg quads x 256 dwords (dword t*16+m of quad q = entry (t, m) of its 4 tables, common.h layout),
-// replicated over the 32 banks. Written as 16-byte units (unit u = LDS bytes 16u..16u+15: super-region
-// u >> 12, row (u >> 8) & 15, column (u >> 4) & 15, half (u >> 3) & 1, lanes 4(u & 7)..+3) by consecutive
-// lanes — conflict-free ds_write_b128 — four units per thread and round with their loads issued together
-// (a quarter of the store instructions and dependent load rounds of dword stores: the 256-thread
-// small-batch kernels staged 3 quads in ~7 us a quad with dword stores). An odd quad count leaves the last
-// super-region's half 1 unwritten (never read).
+// replicated over the 32 banks. Each wave takes chunks of 64 raw dwords (chunk c -> wave c mod waves); all of
+// a lane's raw dwords (up to kStageR chunks) are loaded up front — ONE dependent global round trip — and
+// each chunk is written as 8 rounds of ds_write_b128 in which lanes 8i..8i+7 write the 128 bank copies of
+// raw dword 8·round + i (fetched with a lane shuffle): consecutive 16-byte units, conflict free. The round-5
+// unit loop needed one round trip per 4 units a thread (8 for 3 quads at 256 threads). An odd quad count
+// leaves the last super-region's half 1 unwritten (never read).
+constexpr int kStageR = 4;
+#ifndef IBL_STAGE_UNITS
+#define IBL_STAGE_UNITS 0   // 1: the earlier loop, four 16-byte units per thread and round trip (A/B)
+#endif
 __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, int nreg) {
-  uint4* l4 = reinterpret_cast<uint4*>(lds);
-  const int n = (int)(lds_of_quads(nreg) / 16), bd = blockDim.x;
-  for (int u = threadIdx.x; u < n; u += 4 * bd) {
-    uint32_t w[4];
-    bool ok[4];
+  if constexpr (IBL_STAGE_UNITS) {
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    const int n = (int)(lds_of_quads(nreg) / 16), bd = blockDim.x;
+    for (int u = threadIdx.x; u < n; u += 4 * bd) {
+      uint32_t w[4];
+      bool ok[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int v = u + k * bd, q = ((v >> 12) << 1) | ((v >> 3) & 1);
-      ok[k] = v < n && q < nreg;
-      w[k] = ok[k] ? img[q * 256 + ((v >> 4) & 255)] : 0u;
+      for (int k = 0; k < 4; ++k) {
+        const int v = u + k * bd, q = ((v >> 12) << 1) | ((v >> 3) & 1);
+        ok[k] = v < n && q < nreg;
+        w[k] = ok[k] ? img[q * 256 + ((v >> 4) & 255)] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (ok[k]) l4[u + k * bd] = make_uint4(w[k], w[k], w[k], w[k]);
+    }
+    return;
+  }
+  const int nraw = nreg * 256, lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6, nchunk = (nraw + 63) >> 6;
+  for (int c0 = 0; c0 < nchunk; c0 += kStageR * nwv) {
+    uint32_t v[kStageR];
+#pragma unroll
+    for (int k = 0; k < kStageR; ++k) {
+      const int r = (c0 + wv + k * nwv) * 64 + lane;
+      v[k] = r < nraw ? img[r] : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (ok[k]) l4[u + k * bd] = make_uint4(w[k], w[k], w[k], w[k]);
+    for (int k = 0; k < kStageR; ++k) {
+      const int c = c0 + wv + k * nwv;
+      if (c >= nchunk) break;   // wave-uniform
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int src = 8 * p + (lane >> 3), r = c * 64 + src;
+        const uint32_t w = __shfl(v[k], src, 64);
+        if (r < nraw)
+          *reinterpret_cast<uint4*>(lds + quad_off(r >> 8) + (uint32_t)(r & 255) * 256u + 16u * (uint32_t)(lane & 7)) =
+              make_uint4(w, w, w, w);
+      }
+    }
   }
 }
 
@@ -1064,9 +1094,19 @@ struct TablePrefetch {
     }
     for (int i = threadIdx.x + kPfSrc * blockDim.x; i < nsrc; i += blockDim.x) raw[i] = img[i];
   }
-  // single set, after the phase barrier: replicate into the table quads at LDS address 0
+  // single set, after the phase barrier: replicate the raw buffer (LDS) into the table quads at address 0,
+  // one 16-byte unit per thread and round (unit u: super-region u >> 12, row/column (u >> 4) & 255, half
+  // (u >> 3) & 1; common.h layout) — LDS reads only, so no prefetched round trips are needed
   __device__ __forceinline__ void replicate(uint8_t* lds, const uint32_t* raw) const {
-    stage_tables(lds, raw, nsrc >> 8);
+    const int nreg = nsrc >> 8, n = (int)(lds_of_quads(nreg) / 16);
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    for (int u = threadIdx.x; u < n; u += blockDim.x) {
+      const int q = ((u >> 12) << 1) | ((u >> 3) & 1);
+      if (q < nreg) {
+        const uint32_t w = raw[q * 256 + ((u >> 4) & 255)];
+        l4[u] = make_uint4(w, w, w, w);
+      }
+    }
   }
   // two sets, before the phase barrier: this thread's units straight into the next phase's set, whose
   // quads start at quad fq (unit i = 8 of the 32 bank copies of raw dword i >> 2, common.h layout)
