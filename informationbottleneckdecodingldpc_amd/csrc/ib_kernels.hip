@@ -777,35 +777,37 @@ __device__ __forceinline__ void small_task(const Args& a, int item, SmallIn<MAXD
   x.node = p0;   // position until the fetch reads the node
 }
 
-// Straight-line fetches (no branch around a load, so the compiler's vmcnt waits stay counted and the staging
-// stores wait only for the table loads issued before them): lanes past the task's count repeat its last node,
-// and rows past the degree repeat the last row (cache hits).
 template <int MAXD, bool GATHER>
 __device__ __forceinline__ void cn_small_fetch(const IbFastArgs& a, int item, int lane, SmallIn<MAXD>& x) {
   small_task(a, item, x);
-  const int st = a.info[4 * (x.node + min(lane, x.cnt - 1)) + 1];
+  if (lane >= x.cnt) return;
+  const int st = a.info[4 * (x.node + lane) + 1];
   const uint32_t off = 4u * (uint32_t)x.c;
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
-    const int e = st + min(j, x.d - 1);
-    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
-    x.in[j] = *reinterpret_cast<const uint32_t*>(row + off);
-    x.tg[j] = a.tgt[e];
+    if (j < x.d) {   // wave-uniform
+      const int e = st + j;
+      const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
+      x.in[j] = *reinterpret_cast<const uint32_t*>(row + off);
+      x.tg[j] = a.tgt[e];
+    }
   }
 }
 
 template <int MAXD>
 __device__ __forceinline__ void vn_small_fetch(const IbFastArgs& a, int item, int lane, SmallIn<MAXD>& x) {
   small_task(a, item, x);
-  const int pos = x.node + min(lane, x.cnt - 1);
+  if (lane >= x.cnt) return;
+  const int pos = x.node + lane;
   x.node = a.info[4 * pos];
   const int st = a.info[4 * pos + 1];
   const uint32_t off = 4u * (uint32_t)x.c;
 #pragma unroll
   for (int j = 0; j < MAXD; ++j) {
-    const int e = st + min(j, x.d - 1);
-    x.in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)e * a.ldb + off);
-    x.tg[j] = a.tgt[e];
+    if (j < x.d) {
+      x.in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)(st + j) * a.ldb + off);
+      x.tg[j] = a.tgt[st + j];
+    }
   }
   x.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)x.node * a.ldb + off);
 }
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_cn_small(IbFastArgs a) {
   const int first = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   SmallIn<MAXD> x;
   constexpr bool kPre = IBL_SMALL_PREFETCH && MAXD <= 8;   // MAXD=16 would spill holding an item across the staging
-  if (kPre) cn_small_fetch<MAXD, GATHER>(a, min(first, nitems - 1), lane, x);   // nitems >= 1 (host check)
+  if (kPre && first < nitems) cn_small_fetch<MAXD, GATHER>(a, first, lane, x);
   stage_end(sr, lds, a.img, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
@@ -1000,7 +1002,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_vn_small(IbFastArgs a) {
   const int first = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   SmallIn<MAXD> x;
   constexpr bool kPre = IBL_SMALL_PREFETCH && MAXD <= 8;
-  if (kPre) vn_small_fetch<MAXD>(a, min(first, nitems - 1), lane, x);
+  if (kPre && first < nitems) vn_small_fetch<MAXD>(a, first, lane, x);
   stage_end(sr, lds, a.img, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
@@ -1760,7 +1762,7 @@ hipError_t launch_ib_vn_fast(const IbFastArgs& a, int maxd, int grid, int block,
 }
 int ib_fast_chunk(int maxd) { return maxd <= 8 ? chunkOf<8>() : chunkOf<16>(); }
 static bool ib_small_args_ok(const IbFastArgs& a, bool vn) {
-  return a.task && a.info && a.tgt && a.out && a.img && a.ch8 && (a.in || (!vn && a.gather)) && a.n_tasks >= 1 &&
+  return a.task && a.info && a.tgt && a.out && a.img && a.ch8 && (a.in || (!vn && a.gather)) && a.n_tasks >= 0 &&
          a.nwords >= 1 && 4 * a.nwords <= a.ldb;
 }
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s) {
