@@ -91,42 +91,6 @@ __device__ __forceinline__ bool gate_open(const int32_t* gate, int lane) {
 // unit loop needed one round trip per 4 units a thread (8 for 3 quads at 256 threads). An odd quad count
 // leaves the last super-region's half 1 unwritten (never read).
 constexpr int kStageR = 4;
-// the raw dwords of the first kStageR x waves chunks: loaded by stage_begin, stored by stage_end (which
-// stages any further chunks itself), so a kernel can issue other loads in between
-struct StageRegs {
-  uint32_t v[kStageR];
-};
-__device__ __forceinline__ void stage_chunk_store(uint8_t* lds, uint32_t v, int c, int nraw, int lane) {
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int src = 8 * p + (lane >> 3), r = c * 64 + src;
-    const uint32_t w = __shfl(v, src, 64);
-    if (r < nraw)
-      *reinterpret_cast<uint4*>(lds + quad_off(r >> 8) + (uint32_t)(r & 255) * 256u + 16u * (uint32_t)(lane & 7)) =
-          make_uint4(w, w, w, w);
-  }
-}
-__device__ __forceinline__ void stage_begin(StageRegs& sr, const uint32_t* img, int nreg) {
-  const int nraw = nreg * 256, lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kStageR; ++k) {
-    const int r = (wv + k * nwv) * 64 + lane;
-    sr.v[k] = r < nraw ? img[r] : 0u;
-  }
-}
-__device__ __forceinline__ void stage_end(const StageRegs& sr, uint8_t* lds, const uint32_t* img, int nreg) {
-  const int nraw = nreg * 256, lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6, nchunk = (nraw + 63) >> 6;
-#pragma unroll
-  for (int k = 0; k < kStageR; ++k) {
-    const int c = wv + k * nwv;
-    if (c < nchunk) stage_chunk_store(lds, sr.v[k], c, nraw, lane);   // wave-uniform
-  }
-  for (int c = wv + kStageR * nwv; c < nchunk; c += nwv) {   // beyond the prefetched chunks (not reached for
-    const int r = c * 64 + lane;                              // <= 4 quads at >= 4 waves)
-    stage_chunk_store(lds, r < nraw ? img[r] : 0u, c, nraw, lane);
-  }
-}
 #ifndef IBL_STAGE_UNITS
 #define IBL_STAGE_UNITS 0   // 1: the earlier loop, four 16-byte units per thread and round trip (A/B)
 #endif
@@ -149,9 +113,29 @@ __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint32_t* img, 
     }
     return;
   }
-  StageRegs r;
-  stage_begin(r, img, nreg);
-  stage_end(r, lds, img, nreg);
+  const int nraw = nreg * 256, lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6, nchunk = (nraw + 63) >> 6;
+  for (int c0 = 0; c0 < nchunk; c0 += kStageR * nwv) {
+    uint32_t v[kStageR];
+#pragma unroll
+    for (int k = 0; k < kStageR; ++k) {
+      const int r = (c0 + wv + k * nwv) * 64 + lane;
+      v[k] = r < nraw ? img[r] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kStageR; ++k) {
+      const int c = c0 + wv + k * nwv;
+      if (c >= nchunk) break;   // wave-uniform
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int src = 8 * p + (lane >> 3), r = c * 64 + src;
+        const uint32_t w = __shfl(v[k], src, 64);
+        if (r < nraw)
+          *reinterpret_cast<uint4*>(lds + quad_off(r >> 8) + (uint32_t)(r & 255) * 256u + 16u * (uint32_t)(lane & 7)) =
+              make_uint4(w, w, w, w);
+      }
+    }
+  }
 }
 
 // column images: ncs tables x 16 columns x 2 dwords (entries t < 8, t >= 8) replicated for the 32
@@ -755,75 +739,26 @@ __global__ __launch_bounds__(1024) void ib_dec_fast(IbDecArgs a) {
 // task shape), a word is codewords 8c..8c+7 (one dword of nibbles of every row), each lane gathering its
 // node's rows. Same table images, the fused kernel's node bodies on one dword (cn_word / vn_word /
 // dec_item), the same syndrome: outputs equal the fast path's bit for bit.
-// A small-batch item's inputs: the task's degree d and word c, and per lane (node p0 + lane < p0 + cnt) its
-// input rows' words, output rows and channel word. Fetched apart from the computation so a kernel's first
-// item loads while its tables are being staged (the loads and the staging round trip overlap).
-template <int MAXD>
-struct SmallIn {
-  uint32_t in[MAXD];
-  int tg[MAXD];
-  uint32_t chw;
-  int d, c, cnt, node;
-};
-
-// item = (task, word) of a small-batch launch (dealt round-robin to the grid's waves)
-template <class Args, int MAXD>
-__device__ __forceinline__ void small_task(const Args& a, int item, SmallIn<MAXD>& x) {
-  const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
-  x.c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
-  const int p0 = sload(a.task, 4 * t);
-  x.cnt = sload(a.task, 4 * t + 1);
-  x.d = sload(a.task, 4 * t + 2);
-  x.node = p0;   // position until the fetch reads the node
-}
-
-template <int MAXD, bool GATHER>
-__device__ __forceinline__ void cn_small_fetch(const IbFastArgs& a, int item, int lane, SmallIn<MAXD>& x) {
-  small_task(a, item, x);
-  if (lane >= x.cnt) return;
-  const int st = a.info[4 * (x.node + lane) + 1];
-  const uint32_t off = 4u * (uint32_t)x.c;
+template <int D, bool GATHER>
+__device__ __forceinline__ void cn_small_item(const IbFastArgs& a, uint32_t lane4, int st, int c, bool do_par,
+                                              bool& unsat) {
+  uint32_t in[D], o[D];
+  int tg[D];
+  const uint32_t off = 4u * (uint32_t)c;
 #pragma unroll
-  for (int j = 0; j < MAXD; ++j) {
-    if (j < x.d) {   // wave-uniform
-      const int e = st + j;
-      const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
-      x.in[j] = *reinterpret_cast<const uint32_t*>(row + off);
-      x.tg[j] = a.tgt[e];
-    }
+  for (int j = 0; j < D; ++j) {
+    const int e = st + j;
+    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
+    in[j] = *reinterpret_cast<const uint32_t*>(row + off);
+    tg[j] = a.tgt[e];
+    o[j] = 0;
   }
-}
-
-template <int MAXD>
-__device__ __forceinline__ void vn_small_fetch(const IbFastArgs& a, int item, int lane, SmallIn<MAXD>& x) {
-  small_task(a, item, x);
-  if (lane >= x.cnt) return;
-  const int pos = x.node + lane;
-  x.node = a.info[4 * pos];
-  const int st = a.info[4 * pos + 1];
-  const uint32_t off = 4u * (uint32_t)x.c;
-#pragma unroll
-  for (int j = 0; j < MAXD; ++j) {
-    if (j < x.d) {
-      x.in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)(st + j) * a.ldb + off);
-      x.tg[j] = a.tgt[st + j];
-    }
-  }
-  x.chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)x.node * a.ldb + off);
-}
-
-template <int D>
-__device__ __forceinline__ void cn_small_compute(const IbFastArgs& a, uint32_t lane4, const uint32_t (&in)[D],
-                                                 const int (&tg)[D], int c, bool do_par, bool& unsat) {
-  uint32_t o[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) o[j] = 0;
   if (do_par) {   // parity of (m < T/2) over the inputs, 8 codewords at once (see cn_compute)
     const uint32_t bias = (uint32_t)(8 - a.half) * 0x11111111u;
-    uint32_t p = (D & 1) ? 0x88888888u : 0u;
+    uint32_t x = (D & 1) ? 0x88888888u : 0u;
 #pragma unroll
-    for (int j = 0; j < D; ++j) p ^= in[j] + bias;
-    if (p & 0x88888888u & valid_nib8(a.B - 8 * c)) unsat = true;
+    for (int j = 0; j < D; ++j) x ^= in[j] + bias;
+    if (x & 0x88888888u & valid_nib8(a.B - 8 * c)) unsat = true;
   }
   const uint32_t fbase = slot_off(a.fslot[D]);
   if constexpr (D == 2) {
@@ -849,17 +784,22 @@ __device__ __forceinline__ void cn_small_compute(const IbFastArgs& a, uint32_t l
     if (a.B - 8 * c <= 4) cn_word<D, 4>(lane4, in, fbase, cb, o);
     else cn_word<D>(lane4, in, fbase, cb, o);
   }
-  const uint32_t off = 4u * (uint32_t)c;
 #pragma unroll
   for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
 }
 
 template <int D>
-__device__ __forceinline__ void vn_small_compute(const IbFastArgs& a, uint32_t lane4, const uint32_t (&in)[D],
-                                                 const int (&tg)[D], uint32_t chw, int c) {
-  uint32_t o[D];
+__device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane4, int node, int st, int c) {
+  uint32_t in[D], o[D];
+  int tg[D];
+  const uint32_t off = 4u * (uint32_t)c;
 #pragma unroll
-  for (int j = 0; j < D; ++j) o[j] = 0;
+  for (int j = 0; j < D; ++j) {
+    in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)(st + j) * a.ldb + off);
+    tg[j] = a.tgt[st + j];
+    o[j] = 0;
+  }
+  const uint32_t chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + off);
   if constexpr (D == 1) {
     o[0] = chw;   // degree 1 forwards the channel value (kernels_template_irreg.cl:131-136)
   } else {
@@ -867,62 +807,8 @@ __device__ __forceinline__ void vn_small_compute(const IbFastArgs& a, uint32_t l
     if (a.B - 8 * c <= 4) vn_word<D, 4>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
     else vn_word<D>(lane4, in, chw, slot_off(a.fslot[D]), cb, o);
   }
-  const uint32_t off = 4u * (uint32_t)c;
 #pragma unroll
   for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
-}
-
-// an item of degree D from a prefetched SmallIn, or loaded here (st = the lane's first own-order edge)
-template <int D, int MAXD>
-__device__ __forceinline__ void cn_small_item(const IbFastArgs& a, uint32_t lane4, const SmallIn<MAXD>& x,
-                                              bool do_par, bool& unsat) {
-  uint32_t in[D];
-  int tg[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    in[j] = x.in[j];
-    tg[j] = x.tg[j];
-  }
-  cn_small_compute<D>(a, lane4, in, tg, x.c, do_par, unsat);
-}
-template <int D, bool GATHER>
-__device__ __forceinline__ void cn_small_item_ld(const IbFastArgs& a, uint32_t lane4, int st, int c, bool do_par,
-                                                 bool& unsat) {
-  uint32_t in[D];
-  int tg[D];
-  const uint32_t off = 4u * (uint32_t)c;
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const int e = st + j;
-    const uint8_t* row = GATHER ? a.ch8 + (size_t)a.gather[e] * a.ldb : a.in + (size_t)e * a.ldb;
-    in[j] = *reinterpret_cast<const uint32_t*>(row + off);
-    tg[j] = a.tgt[e];
-  }
-  cn_small_compute<D>(a, lane4, in, tg, c, do_par, unsat);
-}
-template <int D, int MAXD>
-__device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane4, const SmallIn<MAXD>& x) {
-  uint32_t in[D];
-  int tg[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    in[j] = x.in[j];
-    tg[j] = x.tg[j];
-  }
-  vn_small_compute<D>(a, lane4, in, tg, x.chw, x.c);
-}
-template <int D>
-__device__ __forceinline__ void vn_small_item_ld(const IbFastArgs& a, uint32_t lane4, int node, int st, int c) {
-  uint32_t in[D];
-  int tg[D];
-  const uint32_t off = 4u * (uint32_t)c;
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    in[j] = *reinterpret_cast<const uint32_t*>(a.in + (size_t)(st + j) * a.ldb + off);
-    tg[j] = a.tgt[st + j];
-  }
-  const uint32_t chw = *reinterpret_cast<const uint32_t*>(a.ch8 + (size_t)node * a.ldb + off);
-  vn_small_compute<D>(a, lane4, in, tg, chw, c);
 }
 
 // (task, word) items of a small-batch launch, dealt round-robin to the grid's waves; body(pos, c, d) runs
@@ -940,52 +826,26 @@ __device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body
   }
 }
 
-// The per-pass small-batch kernels: the wave's first item is fetched between the table loads and their LDS
-// stores (stage_begin / stage_end), later items one at a time.
-#ifndef IBL_SMALL_PREFETCH
-#define IBL_SMALL_PREFETCH 1   // 0: fetch every item after the staging (A/B, tools/variants.py spf0)
-#endif
 template <int MAXD, bool GATHER>
 __global__ __launch_bounds__(kSmallBlock) void ib_cn_small(IbFastArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
   if (!gate_open(a.gate, lane)) return;
   lds_at_zero(lds);
-  StageRegs sr;
-  stage_begin(sr, a.img, a.nt);
-  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_tasks * a.nwords;
-  const int first = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  SmallIn<MAXD> x;
-  constexpr bool kPre = IBL_SMALL_PREFETCH && MAXD <= 8;   // MAXD=16 would spill holding an item across the staging
-  if (kPre && first < nitems) cn_small_fetch<MAXD, GATHER>(a, first, lane, x);
-  stage_end(sr, lds, a.img, a.nt);
+  stage_tables(lds, a.img, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
   const bool do_par = !GATHER && a.unsat != nullptr;
   bool unsat = false;
-  if constexpr (kPre) {
-    for (int item = first; item < nitems; item += nw) {
-      if (item != first) cn_small_fetch<MAXD, GATHER>(a, item, lane, x);
-      if (lane < x.cnt) {
-        switch (x.d) {
-#define X(D) case D: if constexpr (D <= MAXD) cn_small_item<D, MAXD>(a, lane4, x, do_par, unsat); break;
-          IBL_DEG_CASES8(X)
+  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int st = a.info[4 * pos + 1];
+    switch (d) {
+#define X(D) case D: if constexpr (D <= MAXD) cn_small_item<D, GATHER>(a, lane4, st, c, do_par, unsat); break;
+      IBL_DEG_CASES(X)
 #undef X
-          default: break;
-        }
-      }
+      default: break;
     }
-  } else {
-    small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-      const int st = a.info[4 * pos + 1];
-      switch (d) {
-#define X(D) case D: cn_small_item_ld<D, GATHER>(a, lane4, st, c, do_par, unsat); break;
-        IBL_DEG_CASES(X)
-#undef X
-        default: break;
-      }
-    });
-  }
+  });
   if (do_par && __ballot(unsat) != 0ull && lane == 0)
     atomicOr(&a.unsat[(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1)], 1);
 }
@@ -996,41 +856,19 @@ __global__ __launch_bounds__(kSmallBlock) void ib_vn_small(IbFastArgs a) {
   const int lane = threadIdx.x & 63;
   if (!gate_open(a.gate, lane)) return;
   lds_at_zero(lds);
-  StageRegs sr;
-  stage_begin(sr, a.img, a.nt);
-  const int wpb = blockDim.x >> 6, nw = gridDim.x * wpb, nitems = a.n_tasks * a.nwords;
-  const int first = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  SmallIn<MAXD> x;
-  constexpr bool kPre = IBL_SMALL_PREFETCH && MAXD <= 8;
-  if (kPre && first < nitems) vn_small_fetch<MAXD>(a, first, lane, x);
-  stage_end(sr, lds, a.img, a.nt);
+  stage_tables(lds, a.img, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
-  if constexpr (kPre) {
-    for (int item = first; item < nitems; item += nw) {
-      if (item != first) vn_small_fetch<MAXD>(a, item, lane, x);
-      if (lane < x.cnt) {
-        switch (x.d) {
-          case 1: vn_small_item<1, MAXD>(a, lane4, x); break;
-#define X(D) case D: if constexpr (D <= MAXD) vn_small_item<D, MAXD>(a, lane4, x); break;
-          IBL_DEG_CASES8(X)
+  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
+    const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
+    switch (d) {
+      case 1: vn_small_item<1>(a, lane4, node, st, c); break;
+#define X(D) case D: if constexpr (D <= MAXD) vn_small_item<D>(a, lane4, node, st, c); break;
+      IBL_DEG_CASES(X)
 #undef X
-          default: break;
-        }
-      }
+      default: break;
     }
-  } else {
-    small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-      const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
-      switch (d) {
-        case 1: vn_small_item_ld<1>(a, lane4, node, st, c); break;
-#define X(D) case D: vn_small_item_ld<D>(a, lane4, node, st, c); break;
-        IBL_DEG_CASES(X)
-#undef X
-        default: break;
-      }
-    });
-  }
+  });
 }
 
 __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {

@@ -45,8 +45,6 @@ VARIANTS = {
     "v2l3": ['IBL_SCHED_FILE="ib_sched_v2l3.inc"'],
     # table staging as 16-byte units, four per thread and global round trip (the loop before the shuffle staging)
     "stageu": ["IBL_STAGE_UNITS=1"],
-    # small-batch kernels fetching every item after the table staging (no first-item prefetch)
-    "spf0": ["IBL_SMALL_PREFETCH=0"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1"],
     # timing-only host hooks (IBL_VN_PART, IBL_TRACE_WAVES, IBL_DEBUG_SYNC): not in the product build
