@@ -501,7 +501,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // Variable-pass co-scheduling (see ib_pass): A/B on DVB-S2 B=8192 (tools/ab.sh, 2 reps each, one box):
 // IBL_MIX 0: VN 0.4825 ms / 170.4k cw/s, 1: 0.4709 / 171.5k, 2: 0.4703 / 171.8k, 3: 0.4782 / 171.1k.
 #ifndef IBL_MIX
-#define IBL_MIX 2
+#define IBL_MIX 2   // (superseded by IBL_MIX16 below; kept for the record of the round-2 A/B)
 #endif
 
 // LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
@@ -643,10 +643,15 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
   const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)lds_of_quads(a.nt);
   // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
-  // degree-2/3 variables, few lookups per byte moved) by HBM. The first IBL_MIX quarters of the
+  // degree-2/3 variables, few lookups per byte moved) by HBM. The first IBL_MIX16 sixteenths of the
   // block's waves take the light share first, so both kinds run side by side on every CU; a wave that
-  // exhausts its first share joins the other (two ticket counters).
-  const bool light_first = VN && (int)(threadIdx.x >> 6) * 4 < wpb * IBL_MIX;   // IBL_MIX quarters of the block
+  // exhausts its first share joins the other (two ticket counters). Round 5, quad layout (heavy items
+  // now 0.239 ms alone, light 0.2405 ms, together 0.436 ms; profiles/r05_vn_mix_ab.json): a quarter of
+  // the waves light-first measured VN 0.4205 ms against 0.433 ms for half (the round-2 choice).
+#ifndef IBL_MIX16
+#define IBL_MIX16 4
+#endif
+  const bool light_first = VN && (int)(threadIdx.x >> 6) * 16 < wpb * IBL_MIX16;
 #pragma unroll 1
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)

@@ -23,9 +23,12 @@ VARIANTS = {
     "spill16": ["IBL_LB16=1024"],
     # variable pass co-scheduling: waves with (threadIdx.x >> 8) < IBL_MIX take the light (degree <= 4,
     # HBM-bound) items first, the others the heavy (LDS-bound) ones
-    "mix1": ["IBL_MIX=1"],
-    "mix2": ["IBL_MIX=2"],
-    "mix3": ["IBL_MIX=3"],
+    "mix1": ["IBL_MIX16=4"],
+    "mix2": ["IBL_MIX16=8"],
+    "mix3": ["IBL_MIX16=12"],
+    "mixw2": ["IBL_MIX16=2"],
+    "mixw3": ["IBL_MIX16=3"],
+    "mixw6": ["IBL_MIX16=6"],
     # three light variable items in flight per wave instead of two; round-2 light rows (W=2, depth 3)
     "ld3": ["IBL_LIGHT_DEPTH=3"],
     "lw2": ["IBL_LIGHT_W=2", "IBL_LIGHT_DEPTH=3"],
