@@ -498,11 +498,9 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // ---------------------------------------------------------------------- kernels
 #define IBL_DEG_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)
 #define IBL_DEG_CASES8(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8)
-// Variable-pass co-scheduling (see ib_pass): A/B on DVB-S2 B=8192 (tools/ab.sh, 2 reps each, one box):
-// IBL_MIX 0: VN 0.4825 ms / 170.4k cw/s, 1: 0.4709 / 171.5k, 2: 0.4703 / 171.8k, 3: 0.4782 / 171.1k.
-#ifndef IBL_MIX
-#define IBL_MIX 2   // (superseded by IBL_MIX16 below; kept for the record of the round-2 A/B)
-#endif
+// Variable-pass co-scheduling (see ib_pass, IBL_MIX16): round-2 A/B on DVB-S2 B=8192 (2 reps each, one box),
+// light-first quarters of the block 0: VN 0.4825 ms / 170.4k cw/s, 1: 0.4709 / 171.5k, 2: 0.4703 / 171.8k,
+// 3: 0.4782 / 171.1k; round 5 (quad layout): 1 quarter best (IBL_MIX16 = 4).
 
 // LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
 __device__ __forceinline__ int* lds_counters(const uint8_t* lds, const IbFastArgs& a) {
