@@ -108,7 +108,9 @@ std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::ve
   }
   return info;
 }
-// {first position, count, degree, 0}: runs of at most 64 positions of one degree in a work order
+// {first position, count, degree, contiguous}: runs of at most 64 positions of one degree in a work order;
+// contiguous = st0 + 1 when the run's nodes are consecutive and their own-order edges follow each other
+// (node p0 + k at edge st0 + k·d), else 0 (the IB small-batch kernels then skip the per-lane record load)
 std::vector<int32_t> order_tasks(const std::vector<int32_t>& info) {
   std::vector<int32_t> t;
   const int32_t n = (int32_t)(info.size() / 4);
@@ -116,7 +118,10 @@ std::vector<int32_t> order_tasks(const std::vector<int32_t>& info) {
     const int32_t d = info[4 * p + 2];
     int32_t c = 0;
     while (p + c < n && c < 64 && info[4 * (p + c) + 2] == d) ++c;
-    t.insert(t.end(), {p, c, d, 0});
+    bool contig = true;
+    for (int32_t k = 1; k < c && contig; ++k)
+      contig = info[4 * (p + k)] == info[4 * p] + k && info[4 * (p + k) + 1] == info[4 * p + 1] + k * d;
+    t.insert(t.end(), {p, c, d, contig ? info[4 * p + 1] + 1 : 0});
     p += c;
   }
   return t;

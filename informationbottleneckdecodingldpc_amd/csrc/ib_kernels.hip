@@ -814,9 +814,12 @@ __device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane
   for (int w = 0; w < D; ++w) *reinterpret_cast<uint32_t*>(a.out + (size_t)tg[w] * a.ldb + off) = o[w];
 }
 
-// (task, word) items of a small-batch launch, dealt round-robin to the grid's waves; body(pos, c, d) runs
-// for the lanes whose position lies in the task (pos = this lane's position in the work order)
-template <class Args, class Body>
+// (task, word) items of a small-batch launch, dealt round-robin to the grid's waves; body(node, st, c, d) runs
+// for the lanes whose position lies in the task, with this lane's node and first own-order edge. A task
+// record {first position, count, degree, contiguous} with contiguous = st0 + 1 says its nodes are
+// consecutive with edges st0 + k·d (every DVB-S2 task): the edge then needs no load, and the node (NODE:
+// variable passes) one scalar load per task instead of a vector load per lane after the record's.
+template <bool NODE, class Args, class Body>
 __device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body) {
   const int wpb = blockDim.x >> 6;
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -825,7 +828,18 @@ __device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body
     const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
     const int c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
     const int p0 = sload(a.task, 4 * t), cnt = sload(a.task, 4 * t + 1), d = sload(a.task, 4 * t + 2);
-    if (lane < cnt) body(p0 + lane, c, d);
+    const int st1 = sload(a.task, 4 * t + 3);
+    if (lane < cnt) {
+      int node = 0, st;
+      if (st1 != 0) {   // wave-uniform
+        st = st1 - 1 + lane * d;
+        if constexpr (NODE) node = sload(a.info, 4 * p0) + lane;
+      } else {
+        st = a.info[4 * (p0 + lane) + 1];
+        if constexpr (NODE) node = a.info[4 * (p0 + lane)];
+      }
+      body(node, st, c, d);
+    }
   }
 }
 
@@ -840,8 +854,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_cn_small(IbFastArgs a) {
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
   const bool do_par = !GATHER && a.unsat != nullptr;
   bool unsat = false;
-  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int st = a.info[4 * pos + 1];
+  small_items<false>(a, lane, [&](int, int st, int c, int d) __attribute__((always_inline)) {
     switch (d) {
 #define X(D) case D: if constexpr (D <= MAXD) cn_small_item<D, GATHER>(a, lane4, st, c, do_par, unsat); break;
       IBL_DEG_CASES(X)
@@ -862,8 +875,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_vn_small(IbFastArgs a) {
   stage_tables(lds, a.img, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
-  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
+  small_items<true>(a, lane, [&](int node, int st, int c, int d) __attribute__((always_inline)) {
     switch (d) {
       case 1: vn_small_item<1>(a, lane4, node, st, c); break;
 #define X(D) case D: if constexpr (D <= MAXD) vn_small_item<D>(a, lane4, node, st, c); break;
@@ -882,8 +894,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
   stage_tables(lds, a.img + (size_t)L * a.nt * 256, a.nt);
   __syncthreads();
   const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
-  small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int node = a.info[4 * pos], st = a.info[4 * pos + 1];
+  small_items<true>(a, lane, [&](int node, int st, int c, int d) __attribute__((always_inline)) {
     const uint32_t off = 4u * (uint32_t)c;
     switch (d) {
       case 1: dec_item<1>(a, lane4, node, st, off, 8 * c); break;
