@@ -819,6 +819,9 @@ __device__ __forceinline__ void vn_small_item(const IbFastArgs& a, uint32_t lane
 // record {first position, count, degree, contiguous} with contiguous = st0 + 1 says its nodes are
 // consecutive with edges st0 + k·d (every DVB-S2 task): the edge then needs no load, and the node (NODE:
 // variable passes) one scalar load per task instead of a vector load per lane after the record's.
+#ifndef IBL_SMALL_CONTIG
+#define IBL_SMALL_CONTIG 1   // 0: every lane loads its node record (A/B, tools/variants.py contig0)
+#endif
 template <bool NODE, class Args, class Body>
 __device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body) {
   const int wpb = blockDim.x >> 6;
@@ -828,7 +831,7 @@ __device__ __forceinline__ void small_items(const Args& a, int lane, Body&& body
     const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
     const int c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
     const int p0 = sload(a.task, 4 * t), cnt = sload(a.task, 4 * t + 1), d = sload(a.task, 4 * t + 2);
-    const int st1 = sload(a.task, 4 * t + 3);
+    const int st1 = IBL_SMALL_CONTIG ? sload(a.task, 4 * t + 3) : 0;
     if (lane < cnt) {
       int node = 0, st;
       if (st1 != 0) {   // wave-uniform

@@ -48,6 +48,8 @@ VARIANTS = {
     "v2l3": ['IBL_SCHED_FILE="ib_sched_v2l3.inc"'],
     # table staging as 16-byte units, four per thread and global round trip (the loop before the shuffle staging)
     "stageu": ["IBL_STAGE_UNITS=1"],
+    # small-batch kernels loading every lane's node record (no contiguous task records)
+    "contig0": ["IBL_SMALL_CONTIG=0"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1"],
     # timing-only host hooks (IBL_VN_PART, IBL_TRACE_WAVES, IBL_DEBUG_SYNC): not in the product build
