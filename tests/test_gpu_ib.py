@@ -229,14 +229,17 @@ def test_ib_fused_equals_passes_and_oracle(eng, name, imax, B, match, early, ebn
     np.testing.assert_array_equal(po, ref)
 
 
-@pytest.mark.parametrize("name", ["reg8000", "wlan"])
+@pytest.mark.parametrize("name", ["reg8000", "wlan", "reg39"])
 def test_ib_fused_table_sets(eng, name, wlan_H, monkeypatch):
     """Both table-staging modes of the fused kernel (two LDS table sets where they fit, as for the
-    (3,6) N=8000 code; one set + raw buffer otherwise, forced with IBL_FUSED_DBUF=0) equal the oracle;
+    (3,6) N=8000 code — one quad of tables a pass, the sets in the two halves of one 64-KiB super-region —
+    and the (3,9) N=900 code — two quads a pass, the second set one super-region up; one set + raw buffer
+    otherwise, forced with IBL_FUSED_DBUF=0) equal the oracle;
     B = 4100 gives 513 groups of 8 codewords (a ragged last one), so workgroups run 2-3 groups and the
     set parity carries across the group boundary (also with 4-codeword half groups: 1025 workgroup
     groups)."""
-    H = codes.regular_code(8000, 3, 6, seed=0) if name == "reg8000" else wlan_H
+    H = {"reg8000": lambda: codes.regular_code(8000, 3, 6, seed=0), "wlan": lambda: wlan_H,
+         "reg39": lambda: codes.regular_code(900, 3, 9, seed=0)}[name]()
     g = graph.build_graph(H)
     G = eng.Graph(g, DEV)
     q = UniformQuantizer(sigma2_from_ebn0(1.0, g.R_c), 16)
