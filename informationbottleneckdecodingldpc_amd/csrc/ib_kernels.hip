@@ -160,17 +160,6 @@ __device__ __forceinline__ uint32_t colq(uint32_t w, int k, uint32_t lane4) {
   const uint32_t src = (k & 1) ? ((w >> 4) & 0x0F0F0F0Fu) : (w & 0x0F0F0F0Fu);
   return __builtin_amdgcn_perm(src, lane4, 0x03020000u | ((4u + (uint32_t)(k >> 1)) << 8));
 }
-// the variable bodies' column terms: a loop of 2-codeword groups would build both spread words per group for
-// 2 perms (2.5 ops a term against the extract + merge's 2), so vp = false there (per-pass and small-batch
-// kernels: VN static VALU -5 %, 95 -> 86 VGPRs); the fused kernel's unrolled groups share the spread words
-// (vp = true: its static VALU is 2 % lower with perms). IBL_VN_PERM = 1 forces perms everywhere (A/B).
-#ifndef IBL_VN_PERM
-#define IBL_VN_PERM 0
-#endif
-__device__ __forceinline__ uint32_t colqv(uint32_t w, int k, uint32_t lane4, bool vp) {
-  if (IBL_VN_PERM || vp) return colq(w, k, lane4);
-  return (__builtin_amdgcn_ubfe(w, 4 * k, 4) << kColSh) | lane4;
-}
 
 // all-ones nibbles for the codewords of a word that lie inside the batch
 __device__ __forceinline__ uint32_t valid_nib8(int remaining) {
@@ -424,7 +413,7 @@ template <int D, int NCW = 8>
 __device__ __forceinline__ void vn_word(uint32_t lane4, const uint32_t (&in)[D], uint32_t chw,
                                         uint32_t fbase, const uint32_t (&cb)[4], uint32_t (&outw)[D]) {
 #pragma unroll 1
-  for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0, false);
+  for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, outw, k0);
 }
 
 template <int D, class Buf>
@@ -959,7 +948,7 @@ __device__ __forceinline__ void fused_vn_word(uint32_t lane4, const uint32_t (&i
                                               const uint32_t (&cb)[4], uint32_t (&o)[D]) {
   if constexpr (IBL_FUSED_UNROLL && D <= 4) {
 #pragma unroll
-    for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0, true);
+    for (int k0 = 0; k0 < NCW; k0 += vn_sched_s(D)) vn_group<D>(lane4, in, chw, fbase, cb, o, k0);
   } else {
     vn_word<D, NCW>(lane4, in, chw, fbase, cb, o);
   }

@@ -133,10 +133,7 @@ def emit_body(kind, D, S, L, NC):
     for j in u8_in:
         for s in range(S):
             base = "lane4f" if j == D - 1 else "lane4"
-            if kind == "cn":
-                lines.append(f"  const uint32_t q{j}_{s} = colq(in[{j}], k0 + {s}, {base});")
-            else:   # vp: v_perm_b32 column terms (unrolled groups share the spread words) or extract + merge
-                lines.append(f"  const uint32_t q{j}_{s} = colqv(in[{j}], k0 + {s}, {base}, vp);")
+            lines.append(f"  const uint32_t q{j}_{s} = colq(in[{j}], k0 + {s}, {base});")
     for j in col_in:
         for s in range(S):
             lines.append(f"  const uint64_t C{j}_{s} = colf(nib(in[{j}], k0 + {s}), cb[{j - (D - NC)}]);")
@@ -204,7 +201,7 @@ def main():
     print("                                                         uint32_t (&o)[D], int k0);")
     print("template <int D> __device__ __forceinline__ void vn_group(uint32_t lane4, const uint32_t (&in)[D],")
     print("                                                         uint32_t chw, uint32_t fbase, const uint32_t (&cb)[4],")
-    print("                                                         uint32_t (&o)[D], int k0, bool vp);")
+    print("                                                         uint32_t (&o)[D], int k0);")
     for D in range(3, KMAXD + 1):
         print(f"template <> __device__ __forceinline__ void cn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
         print("                                                         uint32_t fbase, const uint32_t (&cb)[4],")
@@ -214,7 +211,7 @@ def main():
     for D in range(2, KMAXD + 1):
         print(f"template <> __device__ __forceinline__ void vn_group<{D}>(uint32_t lane4, const uint32_t (&in)[{D}],")
         print("                                                         uint32_t chw, uint32_t fbase, const uint32_t (&cb)[4],")
-        print(f"                                                         uint32_t (&o)[{D}], int k0, bool vp) {{")
+        print(f"                                                         uint32_t (&o)[{D}], int k0) {{")
         print("\n".join(emit_body("vn", D, *cfg(Sv, Lv, D), vn_ncols(D, NCv))))
         print("}")
 

@@ -50,8 +50,6 @@ VARIANTS = {
     "stageu": ["IBL_STAGE_UNITS=1"],
     # small-batch kernels loading every lane's node record (no contiguous task records)
     "contig0": ["IBL_SMALL_CONTIG=0"],
-    # variable bodies' column terms as v_perm_b32 too (the default extracts and merges them)
-    "vnperm": ["IBL_VN_PERM=1"],
     # fused IB kernel phase trace (IBL_TRACE_FUSED=<file>)
     "ftrace": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1"],
     # timing-only host hooks (IBL_VN_PART, IBL_TRACE_WAVES, IBL_DEBUG_SYNC): not in the product build
