@@ -188,7 +188,7 @@ struct ibl_ib {
   int32_t *flags = nullptr, *dL = nullptr;
   // fast path
   uint32_t *cn_img = nullptr, *vn_img = nullptr, *dec_img = nullptr;
-  int cn_nt = 0, vn_nt = 0, dec_nt = 0;   // fast path: LDS table regions (4 tables each) per pass
+  int cn_nt = 0, vn_nt = 0, dec_nt = 0;   // fast path: LDS table quads (4 tables each) per pass
   int32_t cn_fslot[kMaxD + 1] = {0}, vn_fslot[kMaxD + 1] = {0};
   uint32_t *cn_cimg = nullptr, *vn_cimg = nullptr;   // column images per pass (ncs x 32 dwords)
   int cn_ncs = 0, vn_ncs = 0;
@@ -390,7 +390,7 @@ std::vector<int> present(const std::vector<int32_t>& deg) {
   return d;
 }
 
-// LDS bytes of a fast CN / VN launch: table regions, column images, the 2 work counters
+// LDS bytes of a fast CN / VN launch: table quads, column images, the 2 work counters
 size_t fast_lds(int nt, int ncs) {
   return lds_of_quads(regions_of(nt)) + (size_t)ncs * kColImg + 64;
 }
@@ -1128,7 +1128,7 @@ int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order) {
 }
 
 // Fused IB decoder eligibility (fast path, no column images, messages + the largest pass's table
-// regions within the CU's LDS, check degree >= 2, an occupancy of >= 1 block without scratch) and
+// quads within the CU's LDS, check degree >= 2, an occupancy of >= 1 block without scratch) and
 // task tables. Leaves fused_ok false when the code does not fit.
 int ib_fused_setup(ibl_ib* h) {
   const ibl_graph* g = h->g;

@@ -95,7 +95,7 @@ struct IbFastArgs {
   int32_t fslot[kMaxD + 1]; // per degree: LDS slot of the final (composite) op
   int32_t nt;               // table quads staged in LDS (4 tables each, common.h layout)
   const uint32_t* cimg;     // this pass's column images: ncs x 16 columns x 2 dwords (stage_cols)
-  int32_t ncs;              // column images staged after the table regions
+  int32_t ncs;              // column images staged after the table quads
   int8_t ccol[kMaxD + 1][4];// per degree: column image of its i-th column-fetched input
   int32_t n_nodes, nchunks, ldb, B, half, match;   // ldb = row stride in BYTES (2 codewords/byte)
   int32_t n_heavy;          // positions [0, n_heavy) have degree > kLightD (item buffer of MAXD rows)
@@ -123,9 +123,9 @@ struct IbDecArgs {
 // Fused on-chip IB decoder (short codes): a workgroup decodes 8 codewords at a time (one dword of
 // 4-bit messages per edge slot, codeword c in nibble c & 7) through ALL iterations with the messages
 // in LDS. Edge slots follow the check-node tasks as in FlFusedArgs; the per-pass table images are the
-// per-pass kernels' (staged into the table region at LDS address 0 before every phase).
+// per-pass kernels' (staged into the table quads at LDS address 0 before every phase).
 struct IbFusedArgs {
-  const uint32_t* cn_img;   // CN tables, pass p = 0..imax-1: cn_nt regions x 256 dwords each
+  const uint32_t* cn_img;   // CN tables, pass p = 0..imax-1: cn_nt quads x 256 dwords each
   const uint32_t* vn_img;   // VN tables, pass k = 0..imax-2
   const uint32_t* dec_img;  // decision tables, pass k = 0..imax-1
   const uint32_t* chT;      // channel nibbles, [group][position] dwords (codewords 8*group .. 8*group+7),
@@ -139,7 +139,7 @@ struct IbFusedArgs {
   const int32_t* dL;        // non-null: re-run to the device stop iteration *dL (skipped if imax-1)
   int32_t cn_fslot[kMaxD + 1], vn_fslot[kMaxD + 1];
   int32_t cn_nt, vn_nt, dec_nt, nreg;   // quads per pass image; nreg = table quads reserved in LDS (per set)
-  int32_t dbuf;             // 1: two table sets of nreg regions (phase p reads set p & 1; the next phase's
+  int32_t dbuf;             // 1: two table sets of nreg quads (phase p reads set p & 1; the next phase's
                             // set is written during the current phase), no raw buffer
   int32_t n_cn_nodes;
   int32_t cn_uni, vn_uni;   // > 0: every task record is {64 t D, min(64, n - 64 t), D, ...} with this D

@@ -502,7 +502,7 @@ __device__ __forceinline__ void dec_item(const IbDecArgs& a, uint32_t lane4, int
 // light-first quarters of the block 0: VN 0.4825 ms / 170.4k cw/s, 1: 0.4709 / 171.5k, 2: 0.4703 / 171.8k,
 // 3: 0.4782 / 171.1k; round 5 (quad layout): 1 quarter best (IBL_MIX16 = 4).
 
-// LDS of the CN / VN kernels: [nt table regions][ncs column images][2 work counters]
+// LDS of the CN / VN kernels: [nt table quads (common.h layout)][ncs column images][2 work counters]
 __device__ __forceinline__ int* lds_counters(const uint8_t* lds, const IbFastArgs& a) {
   return reinterpret_cast<int*>(const_cast<uint8_t*>(lds) + lds_of_quads(a.nt) + (size_t)a.ncs * kColImg);
 }
@@ -638,7 +638,7 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
     *trace_items = (uint64_t)__smid() << 32;
   }
   int* ctr = lds_counters(lds, a);  // 2 phase counters
-  // column images follow the table regions (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
+  // column images follow the table quads (colf: cb = 8*(lane&31) + their base + 4 KiB per image)
   const uint32_t lane8c = ((uint32_t)(lane & 31) << 3) + (uint32_t)lds_of_quads(a.nt);
   // Variable passes: heavy items (degree > kLightD) are bound by the LDS array, light ones (DVB-S2's
   // degree-2/3 variables, few lookups per byte moved) by HBM. The first IBL_MIX16 sixteenths of the
@@ -910,7 +910,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
 }
 
 // ------------------------------------------------------------- fused on-chip decoder
-// For short codes (E * 4 B of messages plus the largest pass's table regions within the CU's LDS,
+// For short codes (E * 4 B of messages plus the largest pass's table quads within the CU's LDS,
 // e.g. regular (3,6) N=8000: 96 KB + 32 KB), one workgroup decodes 8 codewords (a dword of 4-bit
 // messages per edge slot) through ALL iterations without touching HBM for messages: the flooding
 // schedule of decode_OpenCL (discrete_LDPC_decoder_irreg.py:277-333, kernels_template_irreg.cl)
@@ -921,7 +921,7 @@ __global__ __launch_bounds__(kSmallBlock) void ib_dec_small(IbDecArgs a) {
 //   (calc_varnode_output :249-302).
 // The node bodies are the per-pass kernels' (cn_word / vn_word on one dword, the same generated fold
 // schedules, the same table images and matching-composed final slots), so outputs equal the per-pass
-// path's bit for bit. Tables are staged into the region at LDS address 0 before every phase (each
+// path's bit for bit. Tables are staged into the quads at LDS address 0 before every phase (each
 // pass has its own tables). Tasks of up to 64 same-degree nodes (lane = node) are handed to waves by
 // LDS tickets. Early stop is batch-global: pass 1 runs imax-1 iterations and records each CN pass's
 // syndrome in the per-pass path's flag words; finalize_iters turns them into L; pass 2 (dL set)
