@@ -175,9 +175,11 @@ template <> struct RowVec<4> { typedef uint4 T; };
 // caches): 1 = nontemporal loads and stores of the variable pass's rows (the HBM-bound pass). The
 // check pass keeps plain accesses (its registers are at the cap). A/B on one box (tools/ab.sh, DVB-S2
 // B=8192, 2 reps): plain 163.3k cw/s (CN 0.4936 / VN 0.4936 ms), nontemporal 165.3k (0.4888 / 0.4860).
-// IBL_NT_CN: the same for the check pass's row loads (not pass 0's channel gather) and stores (A/B)
+// IBL_NT_CN: the same for the check pass's row loads (not pass 0's channel gather) and stores. Round 4: no
+// gain; round 5 on the quad layout (profiles/r05_c4_nontemporal_cn_quad_ab.json): +0.3-0.7 % (the variable
+// pass after a nontemporal check pass 0.4257-0.427 vs 0.430 ms), so on by default.
 #ifndef IBL_NT_CN
-#define IBL_NT_CN 0
+#define IBL_NT_CN 1
 #endif
 #ifndef IBL_NT
 #define IBL_NT 1

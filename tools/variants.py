@@ -65,6 +65,7 @@ VARIANTS = {
     "flplain": ["IBL_FL_NT=0"],
     # nontemporal check-pass rows (the variable pass's are nontemporal by default)
     "ntcn": ["IBL_NT_CN=1"],
+    "ntcn0": ["IBL_NT_CN=0"],
     # float variable items over 2-KiB row segments (two 16-byte pieces per lane)
     "flvn2": ["IBL_FL_VN2=1"],
     # float kernels built with NaNs not honoured but the IEEE mode bit on
