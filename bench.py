@@ -43,7 +43,8 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip tabl
 CH_SEED = 2              # Philox key of the synthetic channel ("seed 2, keyed by global codeword index")
 
 
-def parse():
+def parse(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -71,12 +72,12 @@ def parse():
                    help="global batch index of rank 0's batch: rank r decodes global batch offset + r, whose channel "
                         "is Philox key 2 at counter (offset + r) * philox_blocks(N, B) (SURVEY H9)")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    a = p.parse_args()
+    a = p.parse_args(argv)
     presets = {"C1": ("regular", "ib", 10, 1000), "C2": ("regular", "ib", 50, 65536),
                "C3": ("wlan", "minsum", 50, 262144), "C4": ("dvbs2", "ib", 50, 8192), "C5": ("dvbs2", "bp", 100, 8192)}
     if a.config:
         a.code, a.kind, a.imax, B = presets[a.config]
-        if "--batch-per-gpu" not in sys.argv:
+        if "--batch-per-gpu" not in argv:
             a.batch_per_gpu = B
         if a.config in ("C1", "C2"):
             a.no_match = True      # Discrete_LDPC_Decoder_class (regular) has no matching step
@@ -459,33 +460,76 @@ def cpu_baseline(a, g, arrays, I, B, match, src, out, code_name):
                       f"{cpu_s:.1f} s wall"}
 
 
+def setup_arrays(a):
+    """Rank 0's setup payload: the code's canonical CSR and random T=16 tables (seed 1) with matching vectors."""
+    from informationbottleneckdecodingldpc_amd import graph, tables
+    g0 = graph.build_graph(make_code(a.code))
+    tb0 = tables.random_tables(16, 16, g0.d_c_max, g0.d_v_max, a.imax, seed=1)
+    return dict(indptr=g0.csr_indptr, cols=g0.csr_cols, shape=np.array([g0.n_c, g0.n_v]),
+                cn=tb0.cn, vn=tb0.vn, mc=tb0.match_cn, mv=tb0.match_vn)
+
+
+def graph_of(arrays):
+    """Host edge graph of the broadcast CSR."""
+    import scipy.sparse as sp
+
+    from informationbottleneckdecodingldpc_amd import graph
+    n_c, n_v = (int(x) for x in arrays["shape"])
+    H = sp.csr_matrix((np.ones(arrays["cols"].size), arrays["cols"], arrays["indptr"]), shape=(n_c, n_v))
+    return graph.build_graph(H)
+
+
+def build_decoder(a, G, g, arrays, q, B):
+    """The decoder a bench run times, from the parsed arguments `a` (the C1-C5 presets), the device graph G,
+    the host graph g, rank 0's broadcast arrays (H and the random tables) and the channel quantiser q.
+    Returns (decoder, match). tests/test_gpu_bench_paths.py builds every config's decoder through this, so
+    the oracle tests run exactly the kernel path each bench line times."""
+    import torch
+
+    from informationbottleneckdecodingldpc_amd import engine, tables
+    I, match = a.imax, not a.no_match
+    if a.kind == "ib":
+        if a.early_stop:
+            # LLR-derived tables (an approximate BP in the T=16 alphabet) so the batch can converge and stop
+            tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, I)
+            match = True
+        else:
+            tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
+        S = a.sub_batch if 0 < a.sub_batch < B else B
+        if B % S:
+            raise SystemExit("--sub-batch must divide the batch")
+        return engine.IBDecoder(G, tb, match, S, path=a.path), match
+    kind = 0 if a.kind == "minsum" else 1
+    return engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.path), match
+
+
+def decoder_path(a, dec, B):
+    """Which kernels decode a batch of B: {"fused", "small", "folded", "name"} — the fused on-chip kernel,
+    the small-batch per-pass kernels (B <= the decoder's small_batch; they do not fold) or the per-pass
+    kernels (float: with `folded` degree-2 variables folded into the check pass)."""
+    fused = dec.fused
+    small = (not fused) and B <= getattr(dec, "small_batch", 0) and (a.kind != "ib" or getattr(dec, "fast_path", False))
+    folded = 0 if (a.kind == "ib" or fused or small) else dec.folded
+    name = "fused on-chip kernel" if fused else ("small-batch per-pass kernels" if small else "per-pass kernels")
+    return {"fused": bool(fused), "small": bool(small), "folded": int(folded), "name": name}
+
+
 def main():
     a = parse()
     import torch
 
-    from informationbottleneckdecodingldpc_amd import codes, distributed, engine, graph, tables
+    from informationbottleneckdecodingldpc_amd import distributed, engine
     from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
 
     rank, world, dev = distributed.init_from_env()
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a HIP device")
     B, I = a.batch_per_gpu, a.imax
-    match = not a.no_match
 
     # ---- setup: rank 0 builds H + tables, one broadcast to every rank (RCCL over xGMI)
-    if rank == 0:
-        H = make_code(a.code)
-        g0 = graph.build_graph(H)
-        tb0 = tables.random_tables(16, 16, g0.d_c_max, g0.d_v_max, I, seed=1)
-        arrays = dict(indptr=g0.csr_indptr, cols=g0.csr_cols, shape=np.array([g0.n_c, g0.n_v]),
-                      cn=tb0.cn, vn=tb0.vn, mc=tb0.match_cn, mv=tb0.match_vn)
-    else:
-        arrays = None
-    arrays = distributed.broadcast_arrays(arrays, src=0)
-    import scipy.sparse as sp
-    n_c, n_v = (int(x) for x in arrays["shape"])
-    H = sp.csr_matrix((np.ones(arrays["cols"].size), arrays["cols"], arrays["indptr"]), shape=(n_c, n_v))
-    g = graph.build_graph(H)
+    arrays = distributed.broadcast_arrays(setup_arrays(a) if rank == 0 else None, src=0)
+    g = graph_of(arrays)
+    n_v = g.n_v
     G = engine.Graph(g, dev)
     q = UniformQuantizer(sigma2_from_ebn0(a.ebn0, g.R_c), 16)
     # channel of global batch gb = batch_offset + rank: the device Philox stream (ibl_channel_sample) under key
@@ -501,17 +545,9 @@ def main():
     def it_slot():
         return its[min(step_k[0], its.numel() - 1):][:1]
 
+    dec, match = build_decoder(a, G, g, arrays, q, B)
     if a.kind == "ib":
-        if early:
-            # LLR-derived tables (an approximate BP in the T=16 alphabet) so the batch can converge and stop
-            tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, I)
-            match = True
-        else:
-            tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
-        S = a.sub_batch if 0 < a.sub_batch < B else B
-        if B % S:
-            raise SystemExit("--sub-batch must divide the batch")
-        dec = engine.IBDecoder(G, tb, match, S, path=a.path)
+        S = dec.max_batch
         ch = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
         engine.channel_sample(ch, q.cdf_t_given_x_equals_zero, CH_SEED, ch_offset)
         out = torch.empty((n_v, B), dtype=torch.uint8, device=dev)
@@ -529,8 +565,6 @@ def main():
         timing_read_fn = L.ibl_ib_timing_read
         w, dtype = 1, "u8"
     else:
-        kind = 0 if a.kind == "minsum" else 1
-        dec = engine.FloatDecoder(G, kind, I, B, precision=torch.float32, path=a.path)
         llr = torch.empty((n_v, B), dtype=torch.float32, device=dev)
         engine.channel_sample(llr, q.cdf_t_given_x_equals_zero, CH_SEED, ch_offset, llr=q.output_LLRs)
         out = torch.empty((n_v, B), dtype=torch.float32, device=dev)
@@ -574,9 +608,8 @@ def main():
     elapsed, value = agg["elapsed_max_s"], agg["value"]
     bpc = bytes_per_cw(g.n_e, n_v, I, w)
     cn_avg, vn_avg = cn_ms / max(cn_n, 1), vn_ms / max(vn_n, 1)
-    fused = dec.fused
-    small = (not fused) and B <= getattr(dec, "small_batch", 0) and (a.kind != "ib" or getattr(dec, "fast_path", False))
-    folded = 0 if (a.kind == "ib" or fused or small) else dec.folded   # the small-batch kernels do not fold
+    kpath = decoder_path(a, dec, B)
+    fused, small, folded = kpath["fused"], kpath["small"], kpath["folded"]
     stop_it = its[:a.steps].cpu().numpy() if a.steps > 0 else np.zeros(1, np.int32)
     fast = a.kind == "ib" and getattr(dec, "fast_path", False)
     # bytes per stored message / channel value as this build moves them: the IB fast path keeps 4-bit
@@ -617,7 +650,7 @@ def main():
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "
                                    f"{B} codewords per GPU, "
                                    f"{('matching ' + ('on' if match else 'off') + ', ') if a.kind == 'ib' else ''}"
-                                   f"{'fused on-chip kernel' if fused else ('small-batch per-pass kernels' if small else 'per-pass kernels')}"
+                                   f"{kpath['name']}"
                                    f"{', early stop on (batch-global)' if early else ', fixed iterations'}",
                        "batch_per_gpu": B, "global_batch": B * world, "imax": I, "parallelism": f"dp{world} batch split",
                        "early_stop": early, "ebn0_db": a.ebn0, "batch_offset": a.batch_offset,

@@ -89,7 +89,13 @@ int ibl_ib_path(const ibl_ib* h);
  * Decode path of an IB decoder on the fast path (no reference counterpart; results are identical):
  *   IBL_PATH_AUTO (default)  the fused on-chip kernel when the code fits (E * 4 bytes of messages
  *                            for 8 codewords plus the largest pass's table quads <= 160 KiB,
- *                            check degrees >= 2; e.g. regular (3,6) N=8000, WLAN), else per-pass;
+ *                            check degrees >= 2; e.g. regular (3,6) N=8000, WLAN), else per-pass.
+ *                            Tables sit in quads of 4 and the quads in 64-KiB super-regions of two,
+ *                            so an odd quad count rounds up (1 quad: 64 KiB, 3 quads: 128 KiB), plus
+ *                            1 KiB of raw image per quad: a code whose largest pass needs 3 quads
+ *                            (9-12 tables) is fused up to E = 7,420 edges (E * 4 <= 29,680 B), 4
+ *                            quads up to 7,164, 1 or 2 quads (<= 8 tables) up to 24,572 / 24,060;
+ *                            the per-pass fast path holds at most 4 quads (16 tables) a pass;
  *   IBL_PATH_PASSES          one launch per check / variable pass, messages in HBM;
  *   IBL_PATH_FUSED           the fused kernel (IBL_EUNSUPPORTED if the code does not fit).
  * ibl_ib_path_in_use reports 1 when decodes run the fused kernel.  With the fused kernel the timing
@@ -152,11 +158,13 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
  * decode_OpenCL_belief_propagation (bp_decoder_irreg.py:221-286).
  *   d_llr [N][B] channel LLRs (IBL_F32 / IBL_F64), d_out [N][B] APP LLRs (IBL_F32 / IBL_F64)
  * Precondition: no channel LLR is NaN.  Min-sum allows +-inf (a known bit: every message a variable
- * sends is clamped to +-llr_max, its APP LLR is +-inf), and every message stays finite.  BP needs finite
- * channel LLRs with |x| <= 354 (the first check pass box-pluses raw channel values; beyond that the
- * reference's fp64 box-plus log((1 + e^(a+b)) / (e^a + e^b)) overflows to NaN, kernels_min_and_BP.cl:5-9);
- * later box-plus inputs are clamped to +-llr_max.  The float kernels take min / max / median as single
- * instructions that assume non-NaN operands: a NaN input gives unspecified outputs.
+ * sends is clamped to +-llr_max, its APP LLR is +-inf), and every message stays finite.  BP box-pluses raw
+ * channel values in the first check pass (later box-plus inputs are clamped to +-llr_max): the fp64 decoder
+ * (the reference's formula log((1 + e^(a+b)) / (e^a + e^b)), kernels_min_and_BP.cl:5-9) needs
+ * |x| <= ln(DBL_MAX) = 709.78 — beyond it e^a overflows and the reference gives NaN; below it an overflowing
+ * numerator or vanishing denominator gives +-inf, clamped to +-llr_max as in the reference — and the fp32
+ * decoder (an overflow-free form of the same function) needs finite values.  The float kernels take min /
+ * max / median as single instructions that assume non-NaN operands: a NaN input gives unspecified outputs.
  */
 int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t B, void* d_out,
                      int32_t out_dtype, int32_t early_stop, int32_t* d_iters, void* stream);
@@ -192,10 +200,14 @@ int ibl_float_set_small_batch(ibl_float* h, int32_t max_b);
 int ibl_float_small_batch(const ibl_float* h, int32_t* max_b);
 /*
  * Channel-LLR precondition check (no reference counterpart).  The staging step of every ibl_float_decode
- * counts the channel LLRs that break ibl_float_decode's precondition — NaN (min-sum); NaN, +-inf or
- * |x| > 354 (BP) — on the device, without a host sync.  This call synchronises `stream`, stores that count
- * since the previous call in *violations (may be NULL), clears it, and returns IBL_EINVAL (message in
- * ibl_last_error) when it is not 0: the outputs of those decodes are unspecified.
+ * counts the channel LLRs that break ibl_float_decode's precondition — NaN (min-sum); NaN or |x| > 709.78
+ * (BP, fp64 decoder); NaN or +-inf (BP, fp32 decoder) — on the device, without a host sync, into one counter
+ * per decoder.  This call synchronises the decoder's DEVICE (every stream: the count covers all decodes of
+ * this decoder enqueued since the previous call, whatever their stream; `stream` is unused), stores that
+ * count in *violations (may be NULL), clears it, and returns IBL_EINVAL (message in ibl_last_error) when it
+ * is not 0: the outputs of those decodes are unspecified.  A caller that wants the verdict of one decode
+ * calls it once before that decode (to clear) and once after (the reference-named classes do so for every
+ * decode that returns host arrays).
  */
 int ibl_float_input_check(ibl_float* h, int32_t* violations, void* stream);
 int ibl_float_timing(ibl_float* h, int32_t enable);

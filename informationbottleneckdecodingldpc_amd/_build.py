@@ -39,8 +39,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB
     src_flags = SRC_FLAGS if src_flags is None else src_flags
     objdir = os.path.join(PKG, "build", tag) if tag else os.path.join(PKG, "build")
     os.makedirs(objdir, exist_ok=True)
-    headers = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "ibldpc.h")] + \
-        [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".inc")]
+    headers = [os.path.join(INCLUDE, "ibldpc.h")] + \
+        [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".inc", ".h"))]
     jobs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)

@@ -22,7 +22,8 @@
 using namespace ibl;
 
 // IBL_DIAG=1 (diagnostic builds, tools/variants.py): the timing-only hooks IBL_VN_PART, IBL_TRACE_WAVES and
-// IBL_TRACE_FUSED. The product build has none of them: no decode call reads the environment.
+// IBL_TRACE_FUSED, and IBL_ALLOW_SCRATCH (create accepts a fast-path build with a private segment). The product
+// build has none of them: no decode call reads the environment, and create always refuses scratch.
 #ifndef IBL_DIAG
 #define IBL_DIAG 0
 #endif
@@ -73,13 +74,9 @@ static int dupload(T** p, const T* h, size_t count) {
   return IBL_OK;
 }
 
-struct ibl_graph {
+struct ibl_graph : HostGraph {   // host copies (plan.h: fold / fused task set-up) + the device arrays
   int device = 0, num_cus = 256;
-  int32_t n_v = 0, n_c = 0;
-  int64_t n_e = 0;
   int32_t dcm = 0, dvm = 0;
-  std::vector<int32_t> h_cn_deg, h_vn_deg;
-  std::vector<int32_t> h_cn_start, h_cols, h_vn_start, h_tgt_vn;   // host copies (fold / fused task set-up)
   int32_t *cn_start = nullptr, *cn_deg = nullptr, *tgt_cn = nullptr;
   int32_t *vn_start = nullptr, *vn_deg = nullptr, *tgt_vn = nullptr, *csr_cols = nullptr;
   // fast-path work order: {node, start, degree, 0} per position, heaviest first (stable)
@@ -90,43 +87,6 @@ struct ibl_graph {
   int32_t n_cn_task = 0, n_vn_task = 0;
 };
 
-namespace {
-std::vector<int32_t> work_order(const std::vector<int32_t>& start, const std::vector<int32_t>& deg, int32_t* heavy) {
-  const int32_t n = (int32_t)deg.size();
-  std::vector<int32_t> idx(n);
-  for (int32_t i = 0; i < n; ++i) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
-  std::vector<int32_t> info(idx.size() * 4);
-  *heavy = 0;
-  for (size_t p = 0; p < idx.size(); ++p) {
-    const int32_t v = idx[p];
-    info[4 * p] = v;
-    info[4 * p + 1] = start[v];
-    info[4 * p + 2] = deg[v];
-    info[4 * p + 3] = 0;
-    if (deg[v] > kLightD) ++*heavy;
-  }
-  return info;
-}
-// {first position, count, degree, contiguous}: runs of at most 64 positions of one degree in a work order;
-// contiguous = st0 + 1 when the run's nodes are consecutive and their own-order edges follow each other
-// (node p0 + k at edge st0 + k·d), else 0 (the IB small-batch kernels then skip the per-lane record load)
-std::vector<int32_t> order_tasks(const std::vector<int32_t>& info) {
-  std::vector<int32_t> t;
-  const int32_t n = (int32_t)(info.size() / 4);
-  for (int32_t p = 0; p < n;) {
-    const int32_t d = info[4 * p + 2];
-    int32_t c = 0;
-    while (p + c < n && c < 64 && info[4 * (p + c) + 2] == d) ++c;
-    bool contig = true;
-    for (int32_t k = 1; k < c && contig; ++k)
-      contig = info[4 * (p + k)] == info[4 * p] + k && info[4 * (p + k) + 1] == info[4 * p + 1] + k * d;
-    t.insert(t.end(), {p, c, d, contig ? info[4 * p + 1] + 1 : 0});
-    p += c;
-  }
-  return t;
-}
-}  // namespace
 
 // HIP-event timing of the CN / VN launches (benchmark only).
 struct KTimer {
@@ -201,6 +161,7 @@ struct ibl_ib {
   int32_t f_ncw_forced = 0;                   // IBL_FUSED_NCW read once at create (A/B, tests), 0 = auto
   // small-batch per-pass kernels (ib_*_small) for B <= small_b (0: off); LDS bytes per launch kind
   int32_t small_b = 0;
+  bool s_ok = false;                          // the small-batch kernels exist for this decoder and run without scratch
   size_t s_lds_cn = 0, s_lds_vn = 0, s_lds_dec = 0;
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
@@ -223,8 +184,10 @@ struct ibl_float {
   void* cin2 = nullptr;
   int32_t *fold = nullptr, *vn_nodes = nullptr;
   int32_t n_vn_nodes = 0, n_folded = 0;
+  std::vector<int32_t> fold_rec, fold_rest;   // the fold's host plan; uploaded with cin2 once a batch can use it
   int32_t* bad = nullptr;   // channel LLRs that violated the precondition since the last ibl_float_input_check
   int32_t small_b = 0;      // small-batch kernels (fl_*_small) for B <= small_b (0: off)
+  bool s_ok = false;        // the small-batch kernels run without scratch (create's check)
   KTimer timer;
   // fused on-chip path (FlFusedArgs): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
@@ -250,36 +213,9 @@ int ibl_device_count(int32_t* n) {
 int ibl_map_node_connections(int32_t n_v, int32_t n_c, const int32_t* indptr, const int32_t* cols,
                              int32_t* cn_start, int32_t* cn_deg, int32_t* tgt_cn, int32_t* vn_start,
                              int32_t* vn_deg, int32_t* tgt_vn) {
-  if (n_v <= 0 || n_c <= 0 || !indptr || !cols) return fail(IBL_EINVAL, "empty graph");
-  if (indptr[0] != 0) return fail(IBL_EINVAL, "csr_indptr[0] must be 0");
-  const int64_t E = indptr[n_c];
-  std::vector<int32_t> vdeg(n_v, 0);
-  for (int32_t c = 0; c < n_c; ++c) {
-    if (indptr[c + 1] < indptr[c]) return fail(IBL_EINVAL, "csr_indptr not monotone");
-    for (int32_t e = indptr[c]; e < indptr[c + 1]; ++e) {
-      if (cols[e] < 0 || cols[e] >= n_v) return fail(IBL_EINVAL, "column index out of range");
-      if (e > indptr[c] && cols[e] <= cols[e - 1])
-        return fail(IBL_EINVAL, "column indices must be strictly ascending within a row (canonical CSR)");
-      vdeg[cols[e]]++;
-    }
-    cn_start[c] = indptr[c];
-    cn_deg[c] = indptr[c + 1] - indptr[c];
-  }
-  int64_t acc = 0;
-  for (int32_t v = 0; v < n_v; ++v) {
-    vn_start[v] = (int32_t)acc;
-    vn_deg[v] = vdeg[v];
-    acc += vdeg[v];
-  }
-  // walking checks in ascending order fills each variable's edges in ascending row order
-  std::vector<int64_t> fill(vn_start, vn_start + n_v);
-  for (int32_t c = 0; c < n_c; ++c)
-    for (int32_t e = indptr[c]; e < indptr[c + 1]; ++e) {
-      const int64_t p = fill[cols[e]]++;
-      tgt_cn[e] = (int32_t)p;
-      tgt_vn[p] = e;
-    }
-  (void)E;
+  std::string err;
+  if (!map_node_connections(n_v, n_c, indptr, cols, cn_start, cn_deg, tgt_cn, vn_start, vn_deg, tgt_vn, &err))
+    return fail(IBL_EINVAL, err);
   return IBL_OK;
 }
 
@@ -605,7 +541,12 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     size_t priv = 0;
     const char* kname = "";
     HIPCHK(ib_fast_private_bytes(CM, VM, &priv, &kname));
-    if (priv != 0 && !getenv("IBL_ALLOW_SCRATCH"))   // diagnostics only (the spill experiment)
+#if IBL_DIAG
+    const bool allow_scratch = getenv("IBL_ALLOW_SCRATCH") != nullptr;   // diagnostic builds: the spill experiment
+#else
+    const bool allow_scratch = false;
+#endif
+    if (priv != 0 && !allow_scratch)
       return bail(fail(IBL_EHIP, std::string("fast-path kernel ") + kname + " has a " + std::to_string(priv) +
                                      "-byte private segment (register spill / scratch item): rebuild required"));
     if ((rc = ib_fused_setup(h))) return bail(rc);
@@ -614,7 +555,8 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
     if (h->cn_ncs == 0 && h->vn_ncs == 0) {
       HIPCHK(ib_small_private_bytes(CM, VM, &priv, &kname));
       const char* sb = getenv("IBL_SMALL_B");
-      h->small_b = priv == 0 ? (sb ? std::max(0, atoi(sb)) : kSmallBatchDefault) : 0;
+      h->s_ok = priv == 0;
+      h->small_b = h->s_ok ? (sb ? std::max(0, atoi(sb)) : kSmallBatchDefault) : 0;
       h->s_lds_cn = lds_of_quads(h->cn_nt);
       h->s_lds_vn = lds_of_quads(h->vn_nt);
       h->s_lds_dec = lds_of_quads(h->dec_nt);
@@ -638,6 +580,8 @@ int ibl_ib_set_small_batch(ibl_ib* h, int32_t max_b) {
   if (max_b < 0) return fail(IBL_EINVAL, "max_b must be >= 0");
   if (max_b > 0 && !(h->fast && h->cn_ncs == 0 && h->vn_ncs == 0 && h->s_lds_cn > 0))
     return fail(IBL_EUNSUPPORTED, "the small-batch kernels need the fast path (T_ch = T_dec <= 16, degrees <= 16)");
+  if (max_b > 0 && !h->s_ok)   // create turned them off: this build's small-batch kernels need scratch
+    return fail(IBL_EUNSUPPORTED, "the small-batch kernels of this build have a private segment: rebuild required");
   h->small_b = max_b;
   return IBL_OK;
 }
@@ -940,48 +884,11 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
 }  // extern "C"
 
 namespace {
-// Task tables of the fused kernels (FlFusedArgs, IbFusedArgs): see below.
-struct FusedTasks {
-  std::vector<int32_t> cn_task, vn_task, vn_node, vn_slot;
-};
-int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order);
 
-// Degree-2 variable fold (FlArgs::fold, fl_cn_item): a degree-2 variable v on checks c1, c2 is folded when
-// both checks have one of their two fold slots free (variables taken in ascending order); each check's record
-// names v's edge position in the check, the check-order row of v's other edge and v. Returns the folded
-// variables' count; `rec` gets n_c records, `rest` the variables the variable pass still updates.
-int32_t plan_fold(const ibl_graph* g, std::vector<int32_t>* rec, std::vector<int32_t>* rest) {
-  const int32_t nc = g->n_c, nv = g->n_v;
-  rec->assign((size_t)nc * kFoldRec, 0);
-  std::vector<int32_t> used(nc, 0);
-  for (int32_t c = 0; c < nc; ++c) (*rec)[(size_t)kFoldRec * c] = (*rec)[(size_t)kFoldRec * c + 1] = -1;
-  // check of each check-order edge
-  std::vector<int32_t> chk_of(g->h_cols.size());
-  for (int32_t c = 0; c < nc; ++c)
-    for (int32_t k = 0; k < g->h_cn_deg[c]; ++k) chk_of[(size_t)g->h_cn_start[c] + k] = c;
-  std::vector<char> folded(nv, 0);
-  int32_t n = 0;
-  for (int32_t v = 0; v < nv; ++v) {
-    if (g->h_vn_deg[v] != 2) continue;
-    const int32_t e1 = g->h_tgt_vn[(size_t)g->h_vn_start[v]], e2 = g->h_tgt_vn[(size_t)g->h_vn_start[v] + 1];
-    const int32_t c1 = chk_of[(size_t)e1], c2 = chk_of[(size_t)e2];
-    if (used[c1] >= 2 || used[c2] >= 2) continue;
-    auto put = [&](int32_t c, int32_t e, int32_t other) {
-      int32_t* r = &(*rec)[(size_t)kFoldRec * c];
-      const int k = used[c]++;
-      r[k] = e - g->h_cn_start[c];
-      r[2 + k] = other;
-      r[4 + k] = v;
-    };
-    put(c1, e1, e2);
-    put(c2, e2, e1);
-    folded[v] = 1;
-    ++n;
-  }
-  rest->clear();
-  for (int32_t v = 0; v < nv; ++v)
-    if (!folded[v]) rest->push_back(v);
-  return n;
+// candidates the fused kernels' bank-order greedy scans per lane (IBL_FUSED_VWIN at create, A/B; default 256)
+size_t fused_vwin() {
+  const char* vw = getenv("IBL_FUSED_VWIN");
+  return (size_t)std::max(1, vw ? atoi(vw) : 256);
 }
 int upload_fused_tasks(const FusedTasks& ft, int32_t** cn_task, int32_t** vn_task, int32_t** vn_node, int32_t** vn_slot) {
   int rc;
@@ -1006,18 +913,8 @@ int fused_setup(ibl_float* h) {
   // code's lanes on runs of consecutive slots, which conflict less than the dword-bank greedy order;
   // IBL_FUSED_VORDER=1 selects the greedy order (A/B)
   const char* voe = getenv("IBL_FUSED_VORDER");
-  if ((rc = build_fused_tasks(g, &ft, voe && voe[0] == '1'))) return rc;
-  // The kernel keeps the variable-edge slot indices in LDS as u16, each variable task's rows at the full
-  // stride of 64 lanes (record field 3 = the task's first padded index): the D index loads of a task share
-  // one address and take their row offsets as immediates, whatever the task's node count.
-  std::vector<int32_t> pslot;
-  for (size_t t = 0; t < ft.vn_task.size() / 4; ++t) {
-    const int32_t cnt = ft.vn_task[4 * t + 1], d = ft.vn_task[4 * t + 2], sf = ft.vn_task[4 * t + 3];
-    ft.vn_task[4 * t + 3] = (int32_t)pslot.size();
-    for (int32_t k = 0; k < d; ++k)
-      for (int32_t i = 0; i < 64; ++i) pslot.push_back(i < cnt ? ft.vn_slot[sf + (size_t)k * cnt + i] : 0);
-  }
-  ft.vn_slot.swap(pslot);
+  build_fused_tasks(*g, &ft, voe && voe[0] == '1', fused_vwin());
+  pad_vn_slots(&ft);
   // messages and channel (16-byte slots), 4 counter words, the padded u16 indices (codes whose indices do
   // not fit beside the messages take the per-pass path)
   const size_t lds = (size_t)(E + g->n_v) * 16 + 16 + ft.vn_slot.size() * 2;
@@ -1037,95 +934,6 @@ int fused_setup(ibl_float* h) {
   return IBL_OK;
 }
 
-// Check nodes sorted by degree (heaviest first, stable) and cut into tasks of up to 64 nodes of one
-// degree; edge k of lane i of a check task gets slot first + k*count + i. Variable nodes likewise;
-// vn_slot maps each variable edge (task-major, k*count + i) to the slot of the same edge. bank_order
-// reorders the variables of each degree for conflict-free dword slot reads (below).
-int build_fused_tasks(const ibl_graph* g, FusedTasks* ft, bool bank_order) {
-  const int64_t E = g->n_e;
-  // candidates the bank-order greedy scans per lane (IBL_FUSED_VWIN at create, A/B; default 256)
-  const char* vw = getenv("IBL_FUSED_VWIN");
-  const size_t vwin = (size_t)std::max(1, vw ? atoi(vw) : 256);
-  const std::vector<int32_t>& tgt_vn = g->h_tgt_vn;
-  auto starts = [](const std::vector<int32_t>& deg) {
-    std::vector<int64_t> st(deg.size() + 1, 0);
-    for (size_t i = 0; i < deg.size(); ++i) st[i + 1] = st[i] + deg[i];
-    return st;
-  };
-  auto sorted = [](const std::vector<int32_t>& deg) {
-    std::vector<int32_t> idx(deg.size());
-    for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int32_t)i;
-    std::stable_sort(idx.begin(), idx.end(), [&](int32_t x, int32_t y) { return deg[x] > deg[y]; });
-    return idx;
-  };
-  const std::vector<int64_t> cst = starts(g->h_cn_deg), vst = starts(g->h_vn_deg);
-  std::vector<int32_t> slot_of((size_t)E);
-  {
-    const std::vector<int32_t> ord = sorted(g->h_cn_deg);
-    int32_t slot = 0;
-    for (size_t i = 0; i < ord.size();) {
-      const int32_t d = g->h_cn_deg[ord[i]];
-      int32_t cnt = 0;
-      while (i + cnt < ord.size() && cnt < 64 && g->h_cn_deg[ord[i + cnt]] == d) ++cnt;
-      ft->cn_task.insert(ft->cn_task.end(), {slot, cnt, d, 0});
-      for (int32_t l = 0; l < cnt; ++l)
-        for (int32_t k = 0; k < d; ++k) slot_of[(size_t)cst[ord[i + l]] + k] = slot + k * cnt + l;
-      slot += cnt * d;
-      i += cnt;
-    }
-  }
-  {
-    std::vector<int32_t> ord = sorted(g->h_vn_deg);
-    // Variable order within each degree: the variable pass reads its edge slots in check-task order,
-    // so lanes of one 32-lane group (one LDS cycle of a ds_read_b32) collide when their k-th slots share
-    // a bank (slot mod 32). Greedily fill each 32-lane group with variables whose k-th slots hit banks
-    // not yet used by the group at that k (scan window 256): the fused IB kernel's dword slots then read
-    // (almost) conflict-free. Any order gives the same results.
-    for (size_t i0 = 0; bank_order && i0 < ord.size();) {
-      const int32_t d = g->h_vn_deg[ord[i0]];
-      size_t i1 = i0;
-      while (i1 < ord.size() && g->h_vn_deg[ord[i1]] == d) ++i1;
-      std::vector<int32_t> pool(ord.begin() + (long)i0, ord.begin() + (long)i1), res;
-      res.reserve(pool.size());
-      auto bank = [&](int32_t v, int k) { return (uint32_t)slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]] & 31u; };
-      while (!pool.empty()) {
-        uint32_t used[kMaxD + 1] = {0};
-        for (int lane = 0; lane < 32 && !pool.empty(); ++lane) {
-          size_t best = 0;
-          int bestc = 1 << 30;
-          const size_t win = std::min<size_t>(pool.size(), vwin);
-          for (size_t c = 0; c < win && bestc > 0; ++c) {
-            int col = 0;
-            for (int k = 0; k < d && k <= kMaxD; ++k) col += (used[k] >> bank(pool[c], k)) & 1u;
-            if (col < bestc) { bestc = col; best = c; }
-          }
-          const int32_t v = pool[best];
-          for (int k = 0; k < d && k <= kMaxD; ++k) used[k] |= 1u << bank(v, k);
-          res.push_back(v);
-          pool.erase(pool.begin() + (long)best);
-        }
-      }
-      std::copy(res.begin(), res.end(), ord.begin() + (long)i0);
-      i0 = i1;
-    }
-    int32_t sidx = 0;
-    for (size_t i = 0; i < ord.size();) {
-      const int32_t d = g->h_vn_deg[ord[i]];
-      int32_t cnt = 0;
-      while (i + cnt < ord.size() && cnt < 64 && g->h_vn_deg[ord[i + cnt]] == d) ++cnt;
-      ft->vn_task.insert(ft->vn_task.end(), {(int32_t)i, cnt, d, sidx});
-      ft->vn_slot.resize((size_t)sidx + (size_t)cnt * d);
-      for (int32_t l = 0; l < cnt; ++l) {
-        const int32_t v = ord[i + l];
-        ft->vn_node.push_back(v);
-        for (int32_t k = 0; k < d; ++k) ft->vn_slot[(size_t)sidx + k * cnt + l] = slot_of[(size_t)tgt_vn[(size_t)vst[v] + k]];
-      }
-      sidx += cnt * d;
-      i += cnt;
-    }
-  }
-  return IBL_OK;
-}
 
 // Fused IB decoder eligibility (fast path, no column images, messages + the largest pass's table
 // quads within the CU's LDS, check degree >= 2, an occupancy of >= 1 block without scratch) and
@@ -1161,9 +969,8 @@ int ib_fused_setup(ibl_ib* h) {
   FusedTasks ft;
   int rc;
   const char* voe = getenv("IBL_FUSED_VORDER");
-  if ((rc = build_fused_tasks(g, &ft, !(voe && voe[0] == '0'))) ||
-      (rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot)))
-    return rc;
+  build_fused_tasks(*g, &ft, !(voe && voe[0] == '0'), fused_vwin());
+  if ((rc = upload_fused_tasks(ft, &h->f_cn_task, &h->f_vn_task, &h->f_vn_node, &h->f_vn_slot))) return rc;
   h->f_ncn = (int32_t)(ft.cn_task.size() / 4);
   h->f_nvn = (int32_t)(ft.vn_task.size() / 4);
   // single-degree sides: task records follow from the task index (IbFusedArgs::cn_uni / vn_uni);
@@ -1194,6 +1001,29 @@ int ib_fused_setup(ibl_ib* h) {
 }
 
 bool ib_fused_in_use(const ibl_ib* h) { return h->fused_ok && h->path != IBL_PATH_PASSES; }
+
+// The fold's device state (second check inbox, per-check records, unfolded variable list) once a batch can reach
+// the per-pass kernels (max_batch > small_b): decoders that only ever run the small-batch kernels — the
+// reference's DVB-S2 driver decodes msg_at_time = 2 — do not hold a fourth E x ldb inbox.
+int fold_alloc(ibl_float* h) {
+  if (h->n_folded == 0 || h->cin2 || h->max_batch <= h->small_b) return IBL_OK;
+  const size_t inbox = (size_t)h->g->n_e * h->ldb * (h->prec == kF32 ? 4 : 8);
+  uint8_t* c2 = nullptr;
+  int rc = dalloc(&c2, inbox);
+  if (rc) return rc;
+  if (hipMemset(c2, 0, inbox) != hipSuccess) {
+    dfree(c2);
+    return fail(IBL_EHIP, "hipMemset failed");
+  }
+  if ((rc = dupload(&h->fold, h->fold_rec.data(), h->fold_rec.size())) ||
+      (rc = dupload(&h->vn_nodes, h->fold_rest.data(), h->fold_rest.size()))) {
+    dfree(c2); dfree(h->fold); dfree(h->vn_nodes);
+    h->fold = h->vn_nodes = nullptr;
+    return rc;
+  }
+  h->cin2 = c2;
+  return IBL_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1211,8 +1041,14 @@ int ibl_float_set_path(ibl_float* h, int32_t path) {
 int ibl_float_set_small_batch(ibl_float* h, int32_t max_b) {
   if (!h) return fail(IBL_EINVAL, "decoder is NULL");
   if (max_b < 0) return fail(IBL_EINVAL, "max_b must be >= 0");
+  if (max_b > 0 && !h->s_ok)   // create turned them off: this build's small-batch kernels need scratch
+    return fail(IBL_EUNSUPPORTED, "the small-batch kernels of this build have a private segment: rebuild required");
+  HIPCHK(hipSetDevice(h->g->device));
+  const int32_t old = h->small_b;
   h->small_b = max_b;
-  return IBL_OK;
+  int rc = fold_alloc(h);   // batches above the new threshold take the per-pass kernels, which fold
+  if (rc) h->small_b = old;
+  return rc;
 }
 
 int ibl_float_small_batch(const ibl_float* h, int32_t* max_b) {
@@ -1229,16 +1065,19 @@ int ibl_float_folded(const ibl_float* h, int32_t* n_folded) {
 
 int ibl_float_input_check(ibl_float* h, int32_t* violations, void* stream) {
   if (!h) return fail(IBL_EINVAL, "decoder is NULL");
-  hipStream_t s = (hipStream_t)stream;
+  // The counter belongs to the decoder and collects every decode's staging, on any stream: synchronise the whole
+  // device (not only `stream`) so no decode still in flight elsewhere adds to it between the read and the clear.
+  (void)stream;
   HIPCHK(hipSetDevice(h->g->device));
+  HIPCHK(hipDeviceSynchronize());
   int32_t n = 0;
-  HIPCHK(hipMemcpyAsync(&n, h->bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemsetAsync(h->bad, 0, sizeof(int32_t), s));
-  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(&n, h->bad, sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(h->bad, 0, sizeof(int32_t)));
   if (violations) *violations = n;
   if (n > 0)
     return fail(IBL_EINVAL, std::to_string(n) + (h->kind == IBL_BP
-                                                     ? " channel LLR(s) NaN, infinite or |x| > 354 (BP precondition)"
+                                                     ? (h->prec == kF64 ? " channel LLR(s) NaN or |x| > 709.78 (BP precondition)"
+                                                                          : " channel LLR(s) NaN or infinite (BP precondition)")
                                                      : " channel LLR(s) NaN (min-sum precondition)") +
                                 ": those decodes' outputs are unspecified");
   return IBL_OK;
@@ -1262,7 +1101,10 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   HIPCHK(hipSetDevice(g->device));
   auto* h = new ibl_float();
   h->g = g; h->kind = kind; h->imax = imax; h->prec = precision; h->max_batch = max_batch; h->llr_max = llr_max;
-  h->ldb = (max_batch + kFlRowPad - 1) / kFlRowPad * kFlRowPad;
+  // rows padded to the widest wave item of the per-pass kernels (fp32 256 / fp64 128 codewords; 512 with IBL_FL_VN2
+  // builds), not beyond: the reference's DVB-S2 driver decodes msg_at_time = 2 in fp64
+  const int pad = std::max(64 * (precision == kF32 ? 4 : 2), fl_vn_chunk(precision, g->dvm));
+  h->ldb = (max_batch + pad - 1) / pad * pad;
   const size_t es = precision == kF32 ? 4 : 8;
   const size_t inbox = (size_t)g->n_e * h->ldb * es;
   int rc;
@@ -1289,20 +1131,13 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
   if (fl_occupancy(1, kind, precision, g->dvm, &bpc) != hipSuccess || bpc < 1) bpc = 1;
   h->grid_vn = std::min(bpc, wcap / fl_block(1, kind, precision, g->dvm)) * g->num_cus;
   if ((rc = fused_setup(h))) return bail(rc);
-  {  // degree-2 variable fold of the per-pass path (IBL_FL_FOLD=0 at create turns it off: A/B)
+  {  // degree-2 variable fold of the per-pass path (IBL_FL_FOLD=0 at create turns it off: A/B); its second check
+     // inbox is allocated only once some batch can reach the per-pass kernels (max_batch > small_b, fold_alloc)
     const char* fe = getenv("IBL_FL_FOLD");
-    std::vector<int32_t> rec, rest;
-    if (!(fe && fe[0] == '0') && (h->n_folded = plan_fold(g, &rec, &rest)) > 0) {
-      h->n_vn_nodes = (int32_t)rest.size();
-      uint8_t* c2 = nullptr;
-      rc = dalloc(&c2, inbox);
-      h->cin2 = c2;
-      if (rc || (rc = dupload(&h->fold, rec.data(), rec.size())) || (rc = dupload(&h->vn_nodes, rest.data(), rest.size())))
-        return bail(rc);
-      if (hipMemset(h->cin2, 0, inbox) != hipSuccess) return bail(fail(IBL_EHIP, "hipMemset failed"));
-    } else {
+    if (!(fe && fe[0] == '0') && (h->n_folded = plan_fold(*g, &h->fold_rec, &h->fold_rest)) > 0)
+      h->n_vn_nodes = (int32_t)h->fold_rest.size();
+    else
       h->n_folded = 0;
-    }
   }
   {  // same guard as the IB fast path: the float kernels are built to run without scratch
     size_t priv = 0;
@@ -1314,8 +1149,10 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
     // small-batch kernels (IBL_SMALL_B at create overrides the default; off if they would need scratch)
     HIPCHK(fl_small_private_bytes(kind, precision, g->dcm, g->dvm, &priv, &kname));
     const char* sb = getenv("IBL_SMALL_B");
-    h->small_b = priv == 0 ? (sb ? std::max(0, atoi(sb)) : kFlSmallBatchDefault) : 0;
+    h->s_ok = priv == 0;
+    h->small_b = h->s_ok ? (sb ? std::max(0, atoi(sb)) : kFlSmallBatchDefault) : 0;
   }
+  if ((rc = fold_alloc(h))) return bail(rc);
   *out = h;
   return IBL_OK;
 }
@@ -1343,7 +1180,9 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   const bool early = early_stop != 0 && I > 1;
   const int cwl = h->prec == kF32 ? 4 : 2;
   const int nchunks = (B + 64 * cwl - 1) / (64 * cwl);
-  const int rule = h->kind == IBL_BP ? 2 : 1;   // the staging kernels count precondition violations
+  // the staging kernels count precondition violations (float_kernels.hip llr_bad): min-sum NaN; BP NaN and, for
+  // the fp64 decoder, |x| > ln(DBL_MAX), for the fp32 decoder +-inf
+  const int rule = h->kind == IBL_BP ? (h->prec == kF64 ? 2 : 3) : 1;
   if (early) HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int32_t) * (size_t)I * kShards, s));
   if (h->fused_ok && h->path != IBL_PATH_PASSES) {
     HIPCHK(launch_fl_stage_t(d_llr, llr_dtype, g->n_v, B, h->f_vn_node, h->chf, h->prec, rule, h->bad, s));
@@ -1439,6 +1278,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
   // variable-inbox row (the decision reads them) and folds nothing. The last iteration's variable pass
   // only feeds a syndrome the reference never reads (its loop ends at imax, bp_decoder_irreg.py:240-268),
   // so it is not run.
+  if (h->n_folded > 0 && !h->cin2) return fail(IBL_EHIP, "fold inbox missing (fold_alloc)");
   const bool fold = h->n_folded > 0;
   void* cb[2] = {fold ? h->cin2 : h->cin, h->cin};
   FlArgs cn{}, vn{};
@@ -1522,34 +1362,6 @@ struct ibl_encoder {
   uint32_t *x = nullptr, *r = nullptr, *t = nullptr, *p = nullptr, *tot = nullptr;
 };
 
-namespace {
-struct Csr {
-  std::vector<int32_t> ip{0}, ix;
-  void push_row(const std::vector<int32_t>& cols) {
-    ix.insert(ix.end(), cols.begin(), cols.end());
-    ip.push_back((int32_t)ix.size());
-  }
-};
-
-// 1 lower / -1 upper triangular with full diagonal, 0 otherwise (LDPC_encoder.py:342-360);
-// rows given as sorted column lists of the square parity part
-int tri_shape(const std::vector<std::vector<int32_t>>& rows) {
-  const int n = (int)rows.size();
-  int64_t nnz = 0, low = 0;
-  for (int i = 0; i < n; ++i) {
-    bool diag = false;
-    for (int c : rows[i]) {
-      ++nnz;
-      if (c <= i) ++low;
-      if (c == i) diag = true;
-    }
-    if (!diag) return 0;
-  }
-  if (low == nnz) return 1;
-  if (low == n) return -1;
-  return 0;
-}
-}  // namespace
 
 extern "C" {
 
@@ -1561,97 +1373,19 @@ int ibl_encoder_create(int32_t n_v, int32_t n_c, const int32_t* indptr, const in
   if (max_batch < 1) return fail(IBL_EINVAL, "max_batch must be >= 1");
   const int32_t N = n_v, M = n_c, K = N - M;
   HIPCHK(hipSetDevice(device));
-  // H = [A | B]; rows of B as column lists relative to K (H is canonical CSR, sorted columns)
-  std::vector<std::vector<int32_t>> brows(M);
-  Csr A;
-  for (int32_t r = 0; r < M; ++r) {
-    std::vector<int32_t> ac;
-    for (int32_t e = indptr[r]; e < indptr[r + 1]; ++e) {
-      const int32_t c = cols[e];
-      if (c < 0 || c >= N) return fail(IBL_EINVAL, "column index out of range");
-      if (c < K) ac.push_back(c); else brows[r].push_back(c - K);
-    }
-    A.push_row(ac);
-  }
+  EncPlan pl;
+  std::string err;
+  const int prc = encoder_plan(N, M, indptr, cols, &pl, &err);
+  if (prc != 0) return fail(prc == -3 ? IBL_EUNSUPPORTED : IBL_EINVAL, err);
   auto* h = new ibl_encoder();
   h->device = device; h->N = N; h->K = K; h->M = M; h->max_batch = max_batch;
   h->Bw = (max_batch + 31) / 32;
-  std::vector<int32_t> order;
-  Csr L, P;
-  auto strict = [&](const std::vector<std::vector<int32_t>>& rows, int dir) {
-    Csr T;
-    for (int i = 0; i < (int)rows.size(); ++i) {
-      std::vector<int32_t> c;
-      for (int j : rows[i])
-        if (dir > 0 ? j < i : j > i) c.push_back(j);
-      T.push_row(c);
-    }
-    return T;
-  };
-  int shape = tri_shape(brows);
-  if (shape != 0) {                                    // (LDPC_encoder.py:208-213)
-    h->algo = shape == 1 ? "Forward Substitution" : "Backward Substitution";
-    h->dir = shape;
-    P = strict(brows, shape);
-  } else {
-    std::vector<std::vector<int32_t>> rev(brows.rbegin(), brows.rend());
-    const int rshape = tri_shape(rev);
-    if (rshape != 0) {                                 // rows reversed (:214-226)
-      h->algo = rshape == 1 ? "Forward Substitution" : "Backward Substitution";
-      h->dir = rshape;
-      for (int i = 0; i < M; ++i) order.push_back(M - 1 - i);
-      P = strict(rev, rshape);
-    } else {                                           // GF(2) factorisation (:227-246, gf2factorize :287-340)
-      if (M > 16384) { delete h; return fail(IBL_EUNSUPPORTED, "GF(2) factorisation limited to 16384 parity bits"); }
-      h->algo = "Matrix Inverse";
-      h->method = 1;
-      const int words = (M + 63) / 64;
-      std::vector<uint64_t> Y2((size_t)M * words, 0), Y1((size_t)M * words, 0);
-      for (int i = 0; i < M; ++i) {
-        for (int c : brows[i]) Y2[(size_t)i * words + (c >> 6)] |= 1ull << (c & 63);
-        Y1[(size_t)i * words + (i >> 6)] |= 1ull << (i & 63);
-      }
-      std::vector<char> used(M, 0);
-      std::vector<int32_t> piv(M, 0);
-      for (int col = 0; col < M; ++col) {
-        const uint64_t bit = 1ull << (col & 63);
-        int pv = -1;
-        for (int i = 0; i < M; ++i)
-          if (!used[i] && (Y2[(size_t)i * words + (col >> 6)] & bit)) {
-            if (pv < 0) { pv = i; continue; }
-            for (int w = 0; w < words; ++w) Y2[(size_t)i * words + w] ^= Y2[(size_t)pv * words + w];
-            Y1[(size_t)i * words + (pv >> 6)] |= 1ull << (pv & 63);
-          }
-        if (pv < 0) { delete h; return fail(IBL_EINVAL, "the last N-K columns of H are singular in GF(2)"); }
-        used[pv] = 1;
-        piv[col] = pv;
-      }
-      auto row_cols = [&](const std::vector<uint64_t>& Y, int i) {
-        std::vector<int32_t> c;
-        for (int w = 0; w < words; ++w)
-          for (uint64_t v = Y[(size_t)i * words + w]; v; v &= v - 1) c.push_back(w * 64 + __builtin_ctzll(v));
-        return c;
-      };
-      std::vector<std::vector<int32_t>> l(M), u(M);
-      for (int i = 0; i < M; ++i) {
-        l[i] = row_cols(Y1, i);
-        u[i] = row_cols(Y2, piv[i]);
-      }
-      L = strict(l, 1);
-      P = strict(u, -1);
-      h->dir = -1;
-      order = piv;
-    }
-  }
-  // bidiagonal P in substitution order -> prefix-XOR scan
-  bool chain = true;
-  for (int i = 0; i < M && chain; ++i) {
-    const int n = P.ip[i + 1] - P.ip[i];
-    const int want = h->dir > 0 ? i - 1 : i + 1;
-    if (want < 0 || want >= M) chain = n == 0;
-    else chain = n == 1 && P.ix[P.ip[i]] == want;
-  }
-  h->chain = chain ? 1 : 0;
+  h->algo = pl.algo;
+  h->method = pl.method;
+  h->dir = pl.dir;
+  h->chain = pl.chain;
+  const Csr &A = pl.A, &L = pl.L, &P = pl.P;
+  const std::vector<int32_t>& order = pl.order;
   auto bail = [&](int rc) { ibl_encoder_destroy(h); return rc; };
   int rc;
   if ((rc = dupload(&h->a_ip, A.ip.data(), A.ip.size())) || (rc = dupload(&h->a_ix, A.ix.data(), A.ix.size())) ||

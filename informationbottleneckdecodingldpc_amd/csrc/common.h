@@ -11,6 +11,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "plan.h"
+
 namespace ibl {
 
 constexpr int kWave = 64;
@@ -59,8 +61,7 @@ constexpr int kColImg = 4096;
 __host__ __device__ constexpr int cn_ncols(int D) { return (D >= 5 && D <= 8) ? IBL_NC_CN : 0; }
 __host__ __device__ constexpr int vn_ncols(int D) { return (D >= 6 && D <= 8) ? IBL_NC_VN : 0; }
 constexpr int kTP = 16;           // IB fast path: alphabet padded to 16 (entry (t,m) at t*16+m)
-constexpr int kMaxD = 16;
-constexpr int kLightD = 4;        // nodes up to this degree run with a 4-row item buffer         // largest node degree with an unrolled fast-path body
+// kMaxD, kLightD, kFoldRec: plan.h
 constexpr int kShards = 64;       // early-stop flag words per iteration (one wave load)
 constexpr int kLdsBytes = 160 * 1024;
 
@@ -207,7 +208,6 @@ struct FlArgs {
   const int32_t* task;
   int32_t n_tasks, nwords;
 };
-constexpr int kFoldRec = 8;
 
 // Fused float decoder: a workgroup keeps Vec<F>::N codewords (one 16-byte slot per edge) entirely
 // in LDS for all iterations. Edge slots are numbered per check-node task (up to 64 check nodes of
@@ -314,7 +314,8 @@ hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int
                               unsigned long long* cnt, hipStream_t s);
 
 hipError_t launch_fl_send(const FlArgs& a, int prec, hipStream_t s);
-// rule: channel-LLR precondition counted into *bad (0 none, 1 NaN, 2 NaN / inf / |x| > 354; float_kernels.hip llr_bad)
+// rule: channel-LLR precondition counted into *bad (0 none, 1 NaN, 2 NaN / |x| > ln(DBL_MAX), 3 NaN / inf as fp32;
+// float_kernels.hip llr_bad)
 hipError_t launch_fl_stage(const void* x, int in_dtype, int n, int B, void* dst, int prec, int ldb, int rule,
                            int32_t* bad, hipStream_t s);
 hipError_t launch_fl_stage_t(const void* x, int in_dtype, int n, int B, const int32_t* perm, void* dst, int prec,

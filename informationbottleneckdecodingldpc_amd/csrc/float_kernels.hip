@@ -695,16 +695,23 @@ __global__ __launch_bounds__(256) void fl_dec(FlDecArgs a) {
   }
 }
 
-// Channel-LLR precondition (ibldpc.h, ibl_float_input_check): rule 1 (min-sum) flags NaN, rule 2 (BP) NaN, +-inf
-// and |x| > 354; rule 0 checks nothing. On the bit pattern of the caller's value: this source is built with
-// -fno-honor-nans, under which a float compare may be folded as if NaN did not exist.
-__device__ __forceinline__ bool llr_bad(float x, int rule) {
-  const uint32_t u = __float_as_uint(x) & 0x7fffffffu;
-  return rule != 0 && u > (rule == 2 ? 0x43b10000u : 0x7f800000u);
-}
+// Channel-LLR precondition (ibldpc.h, ibl_float_input_check), on the bit pattern of the caller's value (this
+// source is built with -fno-honor-nans, under which a float compare may be folded as if NaN did not exist):
+//   rule 0 checks nothing; rule 1 (min-sum) flags NaN;
+//   rule 2 (BP, fp64 decoder) flags NaN and |x| > ln(DBL_MAX) = 709.782712893384: the reference's box-plus
+//     log((1 + e^(a+b)) / (e^a + e^b)) (kernels_min_and_BP.cl:5-9) is NaN only once e^a itself overflows —
+//     below that an infinite numerator or a zero denominator gives +-inf, which the clamp maps to +-llr_max;
+//   rule 3 (BP, fp32 decoder) flags NaN and +-inf of the value the decoder stages (a caller f64 beyond FLT_MAX
+//     rounds to inf): the fp32 box-plus (boxplus(float, ...)) is overflow-free for every finite input.
 __device__ __forceinline__ bool llr_bad(double x, int rule) {
   const uint64_t u = (uint64_t)__double_as_longlong(x) & 0x7fffffffffffffffull;
-  return rule != 0 && u > (rule == 2 ? 0x4076200000000000ull : 0x7ff0000000000000ull);
+  if (rule == 3) return ((uint32_t)__float_as_uint((float)x) & 0x7fffffffu) >= 0x7f800000u;
+  return rule != 0 && u > (rule == 2 ? 0x40862e42fefa39efull : 0x7ff0000000000000ull);
+}
+__device__ __forceinline__ bool llr_bad(float x, int rule) {
+  const uint32_t u = __float_as_uint(x) & 0x7fffffffu;
+  if (rule == 2) return llr_bad((double)x, 2);
+  return rule != 0 && u >= (rule == 3 ? 0x7f800000u : 0x7f800001u);
 }
 // violations counted per lane (rare path: the check itself is one compare per value)
 __device__ __forceinline__ void llr_count(int32_t* bad, int nb) {

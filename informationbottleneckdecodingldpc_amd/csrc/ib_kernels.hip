@@ -8,14 +8,19 @@
 //   calc_varnode_output                                              -> ib_dec_fast
 //
 // Fast path design (T_ch == T_dec <= 16, degrees <= kMaxD):
-//   * messages are u8, [edge][codeword]; a wave item = one node x 256 codewords, 4 codewords
-//     per lane packed in one dword per edge row (coalesced 256-B row segments);
-//   * the pass's lookup tables are staged in LDS, each 16x16 table replicated over the 32
-//     banks (entry e=(t,m) in LDS row e>>2, bank = lane&31, byte e&3), so every ds_read_u8
-//     lookup is bank-conflict free and costs one v_lshl_add (row of t) + one DS op;
+//   * messages are 4-bit nibbles, [edge][codeword] (codeword c in nibble c & 1 of byte c / 2 of its row);
+//     a wave item = one node x 1024 codewords (kChunkIB: a lane owns kW = 2 dwords, 16 codewords, of every
+//     edge row; the max-degree-16 bodies 1 dword), light variable items (degree <= kLightD) 2048 codewords
+//     over 1-KiB row segments (IBL_LIGHT_W); coalesced row segments;
+//   * the pass's lookup tables are staged in LDS in quads of 4 (byte slot & 3 of a dword) and super-
+//     regions of two quads (common.h quad_off / slot_off), each entry replicated over the 32 banks:
+//     entry (t, m) at (t << 12) | (m << 8) | 4 (lane & 31) + slot, so every ds_read_u8 lookup is bank-
+//     conflict free and costs one v_lshl_or_b32 (row t merged with the column term) + one DS op, and a
+//     column term is one v_perm_b32 placing the codeword's nibble in byte 1 of the lane term (colq);
 //   * the order-sensitive folds are computed with prefix sharing (bit-exact: same ops in the
 //     same order as the reference's per-output folds, kernels_template_irreg.cl:205-231),
-//     25 instead of 35 lookups for a degree-7 check, 35 instead of 56 for a degree-8 variable;
+//     25 instead of 35 lookups for a degree-7 check, 35 instead of 56 for a degree-8 variable,
+//     list-scheduled onto concurrent chains by tools/gen_sched.py (ib_sched.inc);
 //   * the matching step (MATCH, :84-91/:162-172/:233-240) is pre-composed on the host into
 //     the final fold table of each degree, so it costs no lookup;
 //   * the syndrome of the batch-global early stop (:304-326 + decoder :310-320) is fused
@@ -29,11 +34,11 @@ namespace ibl {
 
 
 // LDS lookups take a 32-bit LDS byte address. These kernels have no static LDS, so the dynamic
-// array starts at LDS address 0 (checked at kernel entry: lds_at_zero): a lookup is one v_lshl_add
-// (row of t plus the precomputed column term) and one ds_read_u8 whose immediate offset selects
+// array starts at LDS address 0 (checked at kernel entry: lds_at_zero): a lookup is one v_lshl_or
+// (row of t merged with the precomputed column term) and one ds_read_u8 whose immediate offset selects
 // the table — adding the link-time base of the extern array would cost a second VALU op.
 typedef __attribute__((address_space(3))) const uint8_t lds8_t;
-// x = row/column part (one v_lshl_add), c = table slot base: x is made opaque so c stays a top-level
+// x = row/column part (one v_lshl_or), c = table slot base: x is made opaque so c stays a top-level
 // constant and folds into the DS immediate offset instead of being pre-added per input in VGPRs.
 __device__ __forceinline__ uint32_t lu(uint32_t x, uint32_t c) {
   asm("" : "+v"(x));

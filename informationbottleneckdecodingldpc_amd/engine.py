@@ -215,9 +215,10 @@ class FloatDecoder:
         return int(f.value)
 
     def input_violations(self, raise_on_error: bool = True) -> int:
-        """Channel LLRs of the decodes since the last call that broke the precondition (NaN; for BP also
-        +-inf and |x| > 354): synchronises the current stream (``ibl_float_input_check``). Raises
-        :class:`_lib.IBLError` when there were any, unless ``raise_on_error`` is False."""
+        """Channel LLRs of this decoder's decodes since the last call (on any stream) that broke the
+        precondition (NaN; BP fp64 also |x| > 709.78, BP fp32 also +-inf): synchronises the device and clears
+        the count (``ibl_float_input_check``). Raises :class:`_lib.IBLError` when there were any, unless
+        ``raise_on_error`` is False."""
         v = ctypes.c_int32()
         rc = _lib.load().ibl_float_input_check(self._h, ctypes.byref(v), _stream_ptr(self.device))
         if raise_on_error:

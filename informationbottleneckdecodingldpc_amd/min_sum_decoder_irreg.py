@@ -52,11 +52,14 @@ class Min_Sum_Decoder_class_irregular(CodeMixin):
         llr = to_device_input(received_blocks, buffer_in, self.device, (torch.float32, torch.float64))
         if llr.shape[1] > self._dec.max_batch:
             self.init_OpenCL_decoding(llr.shape[1], self.device)
+        if not return_buffer:
+            # host output synchronises anyway: channel LLRs of THIS decode that break the precondition (NaN; BP:
+            # also |x| > 709.78 in fp64, +-inf in fp32) raise instead of returning unspecified values
+            # (FloatDecoder.input_violations); counts left by earlier return_buffer decodes are cleared first
+            self._dec.input_violations(raise_on_error=False)
         out = self._dec.decode(llr, early_stop=early_stop)
         if return_buffer:
             return out
-        # host output synchronises anyway: channel LLRs that break the precondition (NaN; BP: also +-inf,
-        # |x| > 354) raise instead of returning unspecified values (FloatDecoder.input_violations)
         self._dec.input_violations()
         return out.cpu().numpy()
 

@@ -473,10 +473,11 @@ def test_float_fold_absent_without_degree2(eng, reg_H):
 # ------------------------------------------------------------------ channel-LLR precondition check
 @pytest.mark.parametrize("path", ["auto", "passes"])
 def test_float_input_check(eng, wlan_H, path):
-    """ibl_float_input_check (VERDICT r04): the staging kernels count channel LLRs that break
-    ibl_float_decode's precondition — BP: NaN, +-inf, |x| > 354; min-sum: NaN only (+-inf is a known bit) —
-    and the query returns IBL_EINVAL with the count; valid inputs count 0. The BP case with +-inf inputs is
-    the one that failed in round 4 (gpurun_out/r4c2) before the precondition was narrowed."""
+    """ibl_float_input_check (VERDICT r04, ADVICE r05): the staging kernels count channel LLRs that break
+    ibl_float_decode's precondition — BP fp64: NaN, |x| > ln(DBL_MAX) = 709.78 (where the reference's box-plus
+    e^a overflows to NaN); BP fp32: NaN, +-inf (the value the decoder stages); min-sum: NaN only (+-inf is a
+    known bit) — and the query returns IBL_EINVAL with the count; valid inputs count 0. The BP case with +-inf
+    inputs is the one that failed in round 4 (gpurun_out/r4c2) before the precondition was narrowed."""
     from informationbottleneckdecodingldpc_amd._lib import IBLError
     g = graph.build_graph(wlan_H)
     G = eng.Graph(g, DEV)
@@ -487,7 +488,8 @@ def test_float_input_check(eng, wlan_H, path):
     bad_inf = llr.copy()
     bad_inf[pos] = np.where(rng.random(pos.sum()) < 0.8, np.inf, -np.inf)
     big = llr.copy()
-    big[0, :5] = [354.0, -354.0, 354.5, -1e6, 353.9]      # two of these break |x| <= 354
+    # fp64 BP: 709.8, -1e6, 1e30, 1e300 break |x| <= 709.78; fp32 BP: only 1e300 (inf once staged in fp32)
+    big[0, :8] = [709.0, -709.0, 709.8, -1e6, 500.0, 1e30, 1e300, 709.78]
     nan = llr.copy()
     nan[3, 7] = np.nan
     for prec in (torch.float32, torch.float64):
@@ -505,10 +507,47 @@ def test_float_input_check(eng, wlan_H, path):
         ms.decode(torch.from_numpy(bad_inf).to(DEV).to(prec), early_stop=False)
         assert ms.input_violations() == 0                       # +-inf allowed for min-sum
         bp.decode(torch.from_numpy(big).to(DEV).to(torch.float64), early_stop=False)
-        assert bp.input_violations(raise_on_error=False) == 2   # the f64 caller values are checked
+        assert bp.input_violations(raise_on_error=False) == (4 if prec == torch.float64 else 1)
+        bp.decode(torch.from_numpy(big.astype(np.float32)).to(DEV), early_stop=False)   # f32 caller values
+        assert bp.input_violations(raise_on_error=False) == (4 if prec == torch.float64 else 1)
         for dec in (bp, ms):
             dec.decode(torch.from_numpy(nan).to(DEV).to(prec), early_stop=False)
             assert dec.input_violations(raise_on_error=False) == 1
+
+
+def test_bp_large_finite_channel_llrs(eng, wlan_H):
+    """BP takes every channel LLR the reference decodes without NaN. fp64: |x| up to ln(DBL_MAX) —
+    e^(a+b) may overflow (the reference then gets log(inf) = inf, clamped to +-llr_max) while e^a does not — equals
+    the fp64 oracle (1e-9) with no violation counted. fp32 (overflow-free box-plus): any finite value; channel
+    values of +-1e30 decode like +-4000 (beyond any sum of clamped messages, so both clamp to +-llr_max in every
+    message), so every APP LLR other than those channel positions' own equals the +-4000 decode, and theirs keep its
+    sign."""
+    g = graph.build_graph(wlan_H)
+    G = eng.Graph(g, DEV)
+    B = 64
+    llr = _llrs(g, B, 1.5, seed=91)
+    rng = np.random.default_rng(92)
+    pos = rng.random(llr.shape) < 0.02
+    sgn = np.where(rng.random(pos.sum()) < 0.8, 1.0, -1.0)
+    big = llr.copy()
+    big[pos] = sgn * rng.uniform(354.0, 709.78, pos.sum())
+    big[0, :2] = [709.78, 709.78]                           # both inputs of one check near the limit
+    dec = eng.FloatDecoder(G, oracle.BP, 15, B, precision=torch.float64)
+    out = dec.decode(torch.from_numpy(big).to(DEV), early_stop=False)
+    assert dec.input_violations() == 0
+    ref = oracle.float_decode(g, oracle.BP, 15, big)
+    o = out.cpu().numpy()
+    assert not np.isnan(ref).any() and not np.isnan(o).any()
+    np.testing.assert_allclose(o, ref, rtol=1e-15, atol=1e-9)
+    f32 = eng.FloatDecoder(G, oracle.BP, 15, B, precision=torch.float32)
+    huge, clip = llr.astype(np.float32), llr.astype(np.float32)
+    huge[pos], clip[pos] = sgn * np.float32(1e30), sgn * np.float32(4000.0)
+    oh = f32.decode(torch.from_numpy(huge).to(DEV), early_stop=False).cpu().numpy()
+    assert f32.input_violations() == 0
+    oc = f32.decode(torch.from_numpy(clip).to(DEV), early_stop=False).cpu().numpy()
+    assert np.isfinite(oh).all()
+    np.testing.assert_array_equal(oh[~pos], oc[~pos])
+    assert ((oh[pos] < 0) == (oc[pos] < 0)).all()
 
 
 def test_dropin_bp_raises_on_invalid_channel(wlan_H):

@@ -270,6 +270,28 @@ def test_ib_fused_path_selection(eng, wlan_H, dvb_H):
         eng.IBDecoder(D, tbd, True, 64, path="fused")
 
 
+@pytest.mark.parametrize("n,fits", [(800, True), (1000, False)])
+def test_ib_fused_limit_three_quads(eng, n, fits):
+    """with the quad layout an odd quad count takes a whole 64-KiB super-region. A regular (9,12)
+    code without matching needs 10 check tables / 9 decision tables a pass = 3 quads = 128 KiB + 3 KiB of raw
+    images, so the fused kernel takes it up to E * 4 <= 29,680 B (ibldpc.h): N = 800 (E = 7,200) is fused, N = 1000
+    (E = 9,000; fused under the round-4 layout's 96 KiB) runs the per-pass fast path. Both equal the oracle."""
+    g = graph.build_graph(codes.regular_code(n, 9, 12, seed=2))
+    assert g.d_c_max == 12 and g.d_v_max == 9 and g.n_e == 9 * n
+    G = eng.Graph(g, DEV)
+    imax, B = 5, 40
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, imax, seed=n)
+    ch = np.random.default_rng(n).integers(0, 16, (g.n_v, B)).astype(np.int32)
+    ref = oracle.ib_decode(g, tb, ch, match=False)
+    out, _, dec = _run(eng, g, tb, ch, False, False, graph_obj=G)
+    assert dec.fast_path and dec.fused == fits
+    np.testing.assert_array_equal(out, ref)
+    if not fits:
+        from informationbottleneckdecodingldpc_amd._lib import IBLError
+        with pytest.raises(IBLError):
+            eng.IBDecoder(G, tb, False, B, path="fused")
+
+
 def test_ib_early_stop_converging(eng, wlan_H):
     """LLR-quantised tables at good SNR: the batch converges before imax; same stop iteration and
     outputs as the oracle, with matching on."""
