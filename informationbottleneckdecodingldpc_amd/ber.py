@@ -18,6 +18,14 @@ order with the reference's stop rule, so a k-rank sweep counts exactly the frame
 (SURVEY H9). ``max_blocks`` bounds a point (the reference loops until ``min_errors`` however long that
 takes).
 
+Throughput: on a HIP device the batches of a round are pipelined — batch k+1's channel (and,
+encoded, its information bits and codewords) is generated on a side stream into the other half of a double
+buffer while batch k decodes on the caller's stream, batch k's error count runs on the side stream into a
+device vector, and the host reads the counts once per round (``sync_every`` batches) while the next round is
+already enqueued (``_DeviceRunner``). Which frames are counted does not change: the stop rule still walks the
+per-batch counts in global order, so a round decoded past the stop is discarded like the rest of a round
+(``cfg.pipeline=False`` runs the reference's call sequence batch by batch, ``_SyncRunner``).
+
 ``encoded=True`` transmits random encoded codewords instead (the reference's
 ``LDPC_BPSK_Transmitter`` + encoder path, AWGN_Channel_Transmission/LDPC_Transmitter.py:109-125): bits
 from the device Philox stream (key ``(seed, 1)``, disjoint from the channel's ``(seed, 0)``; counter keyed
@@ -55,6 +63,7 @@ class BERConfig:
     sync_every: int = 1                   # batches between cross-rank counter reductions
     llr_dtype: Optional[object] = None    # float decoders: torch dtype of the channel LLRs
     encoded: bool = False                 # random encoded codewords (LDPC_BPSK_Transmitter) instead of all-zero
+    pipeline: bool = True                 # device double buffering + side-stream counts (see the module docstring)
 
 
 @dataclass
@@ -122,6 +131,160 @@ def global_batch(base: int, round_: int, rank: int, world: int) -> int:
     return int(base) + int(round_) * int(world) + int(rank)
 
 
+class _SyncRunner:
+    """The reference driver's call sequence, one batch at a time (DVB-S2/BER_simulation_OpenCL.py:105-112):
+    ``quantize_direct_OpenCL[_LLR]`` -> ``decode_OpenCL*`` -> ``return_errors_all_zero`` (a host sync per batch).
+    Used with ``cfg.pipeline=False`` and for decoder / quantiser objects that are not device-backed."""
+    lookahead = False
+
+    def __init__(self, decoder, kind, quanti, tx, B, N_var, pb_ch, pb_bits, err_rows, thr, cfg):
+        self.decoder, self.kind, self.quanti, self.tx = decoder, kind, quanti, tx
+        self.B, self.N_var, self.pb_ch, self.pb_bits = B, N_var, pb_ch, pb_bits
+        self.err_rows, self.thr, self.cfg = err_rows, thr, cfg
+        if tx is not None:
+            import torch
+            self.cnt = torch.zeros(1, dtype=torch.int64, device=tx.encoder.device)
+
+    def enqueue(self, gs, next_g=None):
+        from .engine import count_errors
+        dec_, q, local = self.decoder, self.quanti, []
+        for g in gs:
+            kw = {}
+            if self.tx is not None:
+                self.tx.offset = g * self.pb_bits
+                kw["bits"] = self.tx.transmit_bits()
+            q.offset = g * self.pb_ch
+            if self.kind == "ib":
+                rec = q.quantize_direct_OpenCL(self.N_var, self.B, **kw)
+                dec = dec_.decode_OpenCL(rec, buffer_in=True, return_buffer=True)
+            else:
+                rec = q.quantize_direct_OpenCL_LLR(self.N_var, self.B, dtype=self.cfg.llr_dtype, **kw)
+                fn = dec_.decode_OpenCL_min_sum if self.kind == "minsum" else dec_.decode_OpenCL_belief_propagation
+                dec = fn(rec, buffer_in=True, return_buffer=True)
+            if self.tx is None:
+                local.append(float(dec_.return_errors_all_zero(dec)))
+            else:
+                local.append(float(count_errors(dec.contiguous(), self.err_rows, self.thr, kw["bits"], self.cnt).item()))
+        return local
+
+    def read(self, handle):
+        return handle
+
+    def finish(self):
+        pass
+
+
+class _DeviceRunner:
+    """Pipelined batches on one HIP device. Per batch k of a round: the side stream generates batch k+1's channel
+    (``ibl_channel_sample`` with the quantiser's CDF / LLRs, seed and the batch's global Philox offset; encoded:
+    ``ibl_random_bits`` + ``ibl_encode`` first) into the free half of a double buffer, once the decode that last
+    read that half is done; the caller's stream waits for batch k's channel and decodes it through the drop-in
+    method (``decode_OpenCL*``, return_buffer); the side stream then counts batch k's errors into slot k of a device
+    vector (the rows and threshold ``return_errors_all_zero`` uses, or the transmitted bits). The host reads a
+    round's vector once (``read``) — by then ``_rank_sweep`` has enqueued the next round. IB channels are u8 cluster
+    ids (the reference's int32 holds the same values; the decoder stages a quarter of the bytes)."""
+    lookahead = True
+
+    def __init__(self, decoder, kind, quanti, tx, B, N_var, pb_ch, pb_bits, err_rows, thr, cfg):
+        import torch
+        self.torch = torch
+        self.decoder, self.kind, self.quanti, self.tx = decoder, kind, quanti, tx
+        self.B, self.pb_ch, self.pb_bits, self.err_rows, self.thr = B, pb_ch, pb_bits, err_rows, thr
+        dev = decoder.device
+        self.dev = dev
+        self.main = torch.cuda.current_stream(dev)
+        self.side = torch.cuda.Stream(dev)
+        ch_dtype = torch.uint8 if kind == "ib" else (cfg.llr_dtype or torch.float64)
+        with torch.cuda.stream(self.side):
+            self.ch = [torch.empty((N_var, B), dtype=ch_dtype, device=dev) for _ in range(2)]
+            if tx is not None:
+                self.info = [torch.empty((tx.K, B), dtype=torch.uint8, device=dev) for _ in range(2)]
+                self.code = [torch.empty((N_var, B), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.side.wait_stream(self.main)        # the buffers exist before the side stream writes them
+        self.used = [None, None]                # event: the decode that last read each half is done
+        self.ready = [None, None]
+        self.slot_g = [None, None]              # global batch whose channel a half holds (None: consumed)
+        self.k = 0
+
+    def _gen(self, slot, g):
+        from .engine import channel_sample, random_bits
+        torch, q = self.torch, self.quanti
+        with torch.cuda.stream(self.side):
+            if self.used[slot] is not None:
+                self.side.wait_event(self.used[slot])
+            bits = None
+            if self.tx is not None:
+                random_bits(self.info[slot], self.tx.seed, g * self.pb_bits)
+                self.tx.encoder.encode_batch(self.info[slot], self.code[slot])
+                bits = self.code[slot]
+            channel_sample(self.ch[slot], q.cdf_t_given_x_equals_zero, q.seed, g * self.pb_ch,
+                           llr=None if self.kind == "ib" else q.output_LLRs, bits=bits)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self.ready[slot], self.slot_g[slot] = ev, g
+
+    def enqueue(self, gs, next_g=None):
+        from .engine import count_below, count_errors
+        torch, d = self.torch, self.decoder
+        with torch.cuda.stream(self.side):
+            cnt = torch.zeros(len(gs), dtype=torch.int64, device=self.dev)
+        for i, g in enumerate(gs):
+            slot = self.k % 2
+            if self.slot_g[slot] != g:
+                self._gen(slot, g)
+            ng = gs[i + 1] if i + 1 < len(gs) else next_g
+            if ng is not None and self.slot_g[1 - slot] != ng:
+                self._gen(1 - slot, ng)         # batch k+1's channel while batch k decodes
+            self.main.wait_event(self.ready[slot])
+            with torch.cuda.stream(self.main):
+                if self.kind == "ib":
+                    dec = d.decode_OpenCL(self.ch[slot], buffer_in=True, return_buffer=True)
+                else:
+                    fn = d.decode_OpenCL_min_sum if self.kind == "minsum" else d.decode_OpenCL_belief_propagation
+                    dec = fn(self.ch[slot], buffer_in=True, return_buffer=True)
+                ev = torch.cuda.Event()
+                ev.record(self.main)
+            self.used[slot], self.slot_g[slot] = ev, None
+            with torch.cuda.stream(self.side):
+                self.side.wait_event(ev)
+                dec.record_stream(self.side)
+                if self.tx is None:
+                    count_below(dec, self.err_rows, self.thr, out=cnt[i:i + 1])
+                else:
+                    count_errors(dec, self.err_rows, self.thr, self.code[slot], out=cnt[i:i + 1])
+            self.k += 1
+        done = torch.cuda.Event()
+        done.record(self.side)
+        return cnt, done
+
+    def read(self, handle):
+        cnt, done = handle
+        done.synchronize()
+        return [float(v) for v in cnt.cpu().tolist()]
+
+    def finish(self):
+        self.torch.cuda.synchronize(self.dev)
+
+
+def _drain(ctx) -> None:
+    """Synchronise `ctx` when it is a HIP device (pipelined batches of another emulated rank may be in flight)."""
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return
+    if isinstance(ctx, torch.device) and ctx.type == "cuda":
+        torch.cuda.synchronize(ctx)
+
+
+def _device_backed(decoder, quanti) -> bool:
+    dev = getattr(decoder, "device", None)
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(dev, torch.device) and dev.type == "cuda" and hasattr(quanti, "cdf_t_given_x_equals_zero")
+
+
 def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: int, log):
     """The Eb/N0 sweep of one rank as a generator: it yields the error counts of the batches it decoded in
     one exchange (``sync_every`` rounds) and is sent back the [world][sync_every] counts of every rank.
@@ -131,10 +294,10 @@ def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: in
     one stream per batch (AWGN_Quantizer_BPSK.py:201-248) and so does the 1-rank run, batch after batch.
     Each rank then walks the exchanged counts in global order and applies the reference's loop condition
     (``while errors < min_errors``, ``DVB-S2/BER_simulation_OpenCL.py:115-121``, plus ``max_blocks``)
-    before each batch; the batches after the stop are discarded (at most world * sync_every - 1 per point)
-    and the next point starts at the first unused global index. A k-rank sweep therefore counts exactly the
-    frames, errors and blocks of the 1-rank sweep with the same per-rank batch, whatever k and
-    ``sync_every`` are."""
+    before each batch; the batches after the stop are discarded (at most world * sync_every - 1 per point, and
+    the device runner's one round of lookahead) and the next point starts at the first unused global index. A
+    k-rank sweep therefore counts exactly the frames, errors and blocks of the 1-rank sweep with the same
+    per-rank batch, whatever k and ``sync_every`` are."""
     from .awgn_quantizer import AWGN_Channel_Quantizer
     from .engine import philox_blocks
     kind = decoder_kind(decoder)
@@ -150,17 +313,14 @@ def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: in
     res = BERResult(np.array([]), np.array([]))
     pb_ch = philox_blocks(N_var, B)
     base = 0                                    # first global batch of the current point
-    tx = None
+    tx, pb_bits = None, 0
+    # rows return_errors_all_zero counts: all N for the regular IB class (:297-300), data_len otherwise
+    err_rows = N_var if type(decoder).__name__ == "Discrete_LDPC_Decoder_class" else int(getattr(decoder, "data_len", N_var))
+    thr = getattr(decoder, "cardinality_T_decoder_ops", 16) // 2 if kind == "ib" else 0.0
     if cfg.encoded:
-        import torch
-        from .engine import count_errors
         from .ldpc_encoder import LDPC_BPSK_Transmitter
         tx = LDPC_BPSK_Transmitter(decoder.H_sparse, B, seed=int(cfg.seed), device=getattr(decoder, "device", None))
         pb_bits = philox_blocks(tx.K, B)
-        # rows return_errors_all_zero counts: all N for the regular IB class (:297-300), data_len otherwise
-        err_rows = N_var if type(decoder).__name__ == "Discrete_LDPC_Decoder_class" else int(decoder.data_len)
-        thr = decoder.cardinality_T_decoder_ops // 2 if kind == "ib" else 0.0
-        cnt = torch.zeros(1, dtype=torch.int64, device=tx.encoder.device)
 
     def more(errors, blocks):
         return errors < cfg.min_errors and (cfg.max_blocks is None or blocks < cfg.max_blocks)
@@ -172,29 +332,28 @@ def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: in
         quanti.seed = int(cfg.seed)
         quanti.offset = base * pb_ch
         quanti.init_OpenCL_quanti(N_var, B, return_buffer_only=True, context_=getattr(decoder, "device", None))
+        _drain(quanti.context)     # a decoder shared by emulated ranks is rebuilt here: nothing may still use it
         decoder.init_OpenCL_decoding(B, quanti.context)
+        run_cls = _DeviceRunner if (cfg.pipeline and _device_backed(decoder, quanti)) else _SyncRunner
+        runner = run_cls(decoder, kind, quanti, tx, B, N_var, pb_ch, pb_bits, err_rows, thr, cfg)
         errors, blocks, used, rnd = 0.0, 0, 0, 0
         t0 = time.time()
+
+        def round_of(r):
+            """This rank's global batches of local rounds r .. r+S-1, and the first batch of the round after (its
+            channel is generated while the round's last batch decodes) unless max_blocks ends the point first."""
+            nxt = None if (cfg.max_blocks is not None and (r + S) * world * B >= cfg.max_blocks) \
+                else global_batch(base, r + S, rank, world)
+            return [global_batch(base, r + s, rank, world) for s in range(S)], nxt
+
+        pending = runner.enqueue(*round_of(rnd)) if more(errors, blocks) else None
         while more(errors, blocks):
-            local = []
-            for s in range(S):
-                g = global_batch(base, rnd + s, rank, world)
-                kw = {}
-                if tx is not None:
-                    tx.offset = g * pb_bits
-                    kw["bits"] = tx.transmit_bits()
-                quanti.offset = g * pb_ch
-                if kind == "ib":
-                    rec = quanti.quantize_direct_OpenCL(N_var, B, **kw)
-                    dec = decoder.decode_OpenCL(rec, buffer_in=True, return_buffer=True)
-                else:
-                    rec = quanti.quantize_direct_OpenCL_LLR(N_var, B, dtype=cfg.llr_dtype, **kw)
-                    fn = decoder.decode_OpenCL_min_sum if kind == "minsum" else decoder.decode_OpenCL_belief_propagation
-                    dec = fn(rec, buffer_in=True, return_buffer=True)
-                if tx is None:
-                    local.append(float(decoder.return_errors_all_zero(dec)))
-                else:
-                    local.append(float(count_errors(dec.contiguous(), err_rows, thr, kw["bits"], cnt).item()))
+            nxt = None
+            # the next round goes to the device before this round's counts are read, unless max_blocks already
+            # ends the point with this round
+            if runner.lookahead and (cfg.max_blocks is None or blocks + S * world * B < cfg.max_blocks):
+                nxt = runner.enqueue(*round_of(rnd + S))
+            local = runner.read(pending)
             counts = yield local
             stop = False
             for s in range(S):                  # global order: round-major, rank-minor
@@ -208,6 +367,8 @@ def _rank_sweep(decoder, cfg: BERConfig, quantizer_factory, rank: int, world: in
                 if stop:
                     break
             rnd += S
+            pending = nxt if nxt is not None else (runner.enqueue(*round_of(rnd)) if more(errors, blocks) else None)
+        runner.finish()
         base += used
         spent = time.time() - t0
         ber[-1] = errors / (R_c * blocks * N_var) if blocks else 0.0

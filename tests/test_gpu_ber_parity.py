@@ -174,3 +174,42 @@ def test_bp_c5_sweep_world_size_invariant(dvb_H):
     for r in (one, two, three):
         _assert_same(r, ref)
     assert ref[3][0] < cfg.max_blocks and ref[3][-1] == cfg.max_blocks   # both stop rules exercised
+
+
+@pytest.mark.parametrize("case", ["ib", "ib_encoded", "bp32", "lockstep2"])
+def test_pipelined_driver_equals_sync_driver(case, wlan_H, dvb_H):
+    """the pipelined BER driver (``_DeviceRunner``: channel of batch k+1 generated on a side stream
+    into a double buffer while batch k decodes, error counts on the side stream, counts read once per round with the
+    next round already enqueued) counts exactly the frames and errors of the reference call sequence
+    (``cfg.pipeline=False``: quantise -> decode -> return_errors_all_zero per batch) — min_errors stops inside a
+    round (the lookahead round is discarded), max_blocks ends the last points; encoded codewords; BP fp32; two
+    emulated ranks sharing one decoder."""
+    from informationbottleneckdecodingldpc_amd.ber import run_ber_lockstep
+    from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
+    from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
+        Discrete_LDPC_Decoder_class_irregular
+    H = dvb_H if case == "bp32" else wlan_H
+    g = graph.build_graph(H)
+    B = 8 if case == "bp32" else 64
+    kw = dict(EbN0_dB_start=0.5, EbN0_dB_max_value=2.0, EbN0_dB_normal_stepwidth=0.5, EbN0_dB_small_stepwidth=0.25,
+              target_error_rate=1e-9, min_errors=3000 if case != "bp32" else 2500, msg_at_time=B,
+              max_blocks=20 * B, seed=17, sync_every=3, encoded=case == "ib_encoded")
+    if case == "bp32":
+        dec = BeliefPropagationDecoderClassIrregular(H, 30, 16, B, precision=torch.float32)
+        kw["llr_dtype"] = torch.float32
+        kw["EbN0_dB_max_value"], kw["EbN0_dB_normal_stepwidth"] = 1.0, 0.25
+    else:
+        design = _quanti(BERConfig(), 10 ** (-1.5 / 10) / (2 * g.R_c))
+        tb = tables.llr_tables(design.output_LLRs, g.d_c_max, g.d_v_max, 15)
+        dec = Discrete_LDPC_Decoder_class_irregular(H, 15, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
+                                                    match="true")
+    res = {}
+    for pipe in (True, False):
+        cfg = BERConfig(**kw, pipeline=pipe)
+        res[pipe] = run_ber_lockstep(dec, cfg, 2) if case == "lockstep2" else run_ber(dec, cfg)
+    a, b = res[True], res[False]
+    print(f"{case}: points {list(b.EbN0_dB_vector)} errors {b.errors} blocks {b.blocks}")
+    assert a.errors == b.errors and a.blocks == b.blocks
+    np.testing.assert_array_equal(a.BER_vector, b.BER_vector)
+    np.testing.assert_array_equal(a.EbN0_dB_vector, b.EbN0_dB_vector)
+    assert len(b.blocks) >= 3 and b.blocks[0] < kw["max_blocks"] and b.blocks[-1] == kw["max_blocks"]
