@@ -7,9 +7,10 @@ channel stream (``oracle.channel_sample``), decoded by the oracle (``oracle.ib_d
 ``oracle.float32_decode``, early stop on, as ``decode_OpenCL*`` do). Bar: identical Eb/N0 points,
 per-point error and block counts, and BER vectors.
 
-Table values: LLR-quantised tables (``tables.llr_tables``) stand in for the reference's IB-designed
-``.pkl`` tables, which need the absent ``ib_base`` package — parity with the published decoders'
-curves is unpinned; parity here is HIP path vs oracle on the same tables and channel.
+Table values: discrete-density-evolution tables (``tables.de_tables``, per-iteration alphabets and
+matching, round 6) stand in for the reference's IB-designed ``.pkl`` tables, which need the absent
+``ib_base`` package — parity with the published decoders' curves is unpinned; parity here is HIP path
+vs oracle on the same tables and channel.
 """
 import numpy as np
 import pytest
@@ -75,7 +76,8 @@ def test_ib_ber_curve_equals_oracle(name, imax, B, max_blocks, start, stop, step
                     EbN0_dB_small_stepwidth=step / 2, target_error_rate=1e-9, min_errors=10 ** 9,
                     msg_at_time=B, max_blocks=max_blocks, seed=11)
     design = _quanti(cfg, 10 ** (-1.5 / 10) / (2 * g.R_c))       # tables designed at 1.5 dB
-    tb = tables.llr_tables(design.output_LLRs, g.d_c_max, g.d_v_max, imax)
+    rho, lam = tables.edge_degree_distributions(g)               # per-iteration DE alphabets (round 6)
+    tb = tables.de_tables(design.p_t_given_x_equals_zero, design.output_LLRs, rho, lam, imax)
     dec = Discrete_LDPC_Decoder_class_irregular(H, imax, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
                                                 match="true")
     r = run_ber(dec, cfg)
@@ -192,7 +194,7 @@ def test_pipelined_driver_equals_sync_driver(case, wlan_H, dvb_H):
     g = graph.build_graph(H)
     B = 8 if case == "bp32" else 64
     kw = dict(EbN0_dB_start=0.5, EbN0_dB_max_value=2.0, EbN0_dB_normal_stepwidth=0.5, EbN0_dB_small_stepwidth=0.25,
-              target_error_rate=1e-9, min_errors=3000 if case != "bp32" else 2500, msg_at_time=B,
+              target_error_rate=1e-9, min_errors=3000 if case != "bp32" else 20000, msg_at_time=B,
               max_blocks=20 * B, seed=17, sync_every=3, encoded=case == "ib_encoded")
     if case == "bp32":
         dec = BeliefPropagationDecoderClassIrregular(H, 30, 16, B, precision=torch.float32)
