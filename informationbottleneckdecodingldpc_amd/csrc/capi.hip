@@ -9,6 +9,7 @@
 // are all zero, and a one-wave kernel turns the flags into the iteration index the output
 // pass uses.  The host only enqueues.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <functional>
 #include <cstdlib>
@@ -1333,7 +1334,10 @@ int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t
   if ((out_dtype == kF32 || out_dtype == kF64) && !llr) return fail(IBL_EINVAL, "LLR output needs llr[T]");
   if (out_dtype == kU8 && T > 256) return fail(IBL_EINVAL, "u8 output needs T <= 256");
   ChArgs a{};
-  for (int w = 0; w <= T; ++w) a.cdf[w] = cdf[w];
+  for (int w = 0; w <= T; ++w) {   // exact: scaling by 2^53 is exact in double; cdf outside [0, 1] saturates
+    const double c = std::ldexp(cdf[w], 53);
+    a.kthr[w] = std::isnan(c) ? ~0ull : (c <= 0.0 ? 0ull : (c >= 18446744073709551615.0 ? ~0ull : (uint64_t)std::floor(c)));
+  }
   if (llr)
     for (int w = 0; w < T; ++w) a.llr[w] = llr[w];
   a.ctr[0] = offset;

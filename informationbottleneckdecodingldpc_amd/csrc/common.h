@@ -284,7 +284,7 @@ hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* d
 // ------------------------------------------------------------ channel generation
 constexpr int kMaxT = 64;         // largest channel alphabet of ibl_channel_sample
 struct ChArgs {
-  double cdf[kMaxT + 1];    // p(t | x = 0) CDF, cdf[0] = 0
+  uint64_t kthr[kMaxT + 1]; // floor(cdf[w] * 2^53) of the p(t | x = 0) CDF: u = m 2^-53 > cdf[w] <=> m > kthr[w]
   double llr[kMaxT];        // output_LLRs (LLR outputs)
   uint64_t ctr[4];          // Philox counter before the batch (numpy Philox `counter`)
   uint64_t key[2];          // Philox key (numpy Philox `key`)

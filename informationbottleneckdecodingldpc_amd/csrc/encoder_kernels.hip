@@ -153,27 +153,6 @@ __global__ void random_bits(uint64_t seed, uint64_t offset, int64_t total, uint8
   }
 }
 
-__global__ void count_errors(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
-                             const uint8_t* bits, int64_t bits_ld, unsigned long long* cnt) {
-  unsigned long long c = 0;
-  const int64_t total = rows * (int64_t)B;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / B, b = i - r * B;
-    const int64_t k = r * ld + b;
-    double v;
-    switch (dtype) {
-      case kU8: v = reinterpret_cast<const uint8_t*>(x)[k]; break;
-      case kI32: v = reinterpret_cast<const int32_t*>(x)[k]; break;
-      case kF32: v = reinterpret_cast<const float*>(x)[k]; break;
-      default: v = reinterpret_cast<const double*>(x)[k]; break;
-    }
-    const bool one = v < thr;                 // decided bit 1 (cluster < T/2, LLR < 0)
-    c += (one != (bits[r * bits_ld + b] != 0)) ? 1ull : 0ull;
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
-}
-
 // -------------------------------------------------------------------- launchers
 static int grid_for(int64_t total) { return (int)std::min<int64_t>(std::max<int64_t>((total + 255) / 256, 1), 8192); }
 
@@ -210,12 +189,6 @@ hipError_t launch_enc_unpack(const uint8_t* info, const uint32_t* p, int K, int 
 }
 hipError_t launch_random_bits(uint64_t seed, uint64_t offset, int64_t total, uint8_t* out, hipStream_t s) {
   hipLaunchKernelGGL(random_bits, dim3(grid_for((total + 3) / 4)), dim3(256), 0, s, seed, offset, total, out);
-  return hipGetLastError();
-}
-hipError_t launch_count_errors(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
-                               const uint8_t* bits, int64_t bits_ld, unsigned long long* cnt, hipStream_t s) {
-  hipLaunchKernelGGL(count_errors, dim3(grid_for(rows * B)), dim3(256), 0, s, x, dtype, rows, B, ld, thr, bits,
-                     bits_ld, cnt);
   return hipGetLastError();
 }
 

@@ -1574,26 +1574,6 @@ __global__ void finalize_iters(const int32_t* flags, int imax, int early, int32_
   }
 }
 
-__global__ void count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
-                            unsigned long long* cnt) {
-  unsigned long long c = 0;
-  const int64_t total = rows * (int64_t)B;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / B, b = i - r * B;
-    const int64_t k = r * ld + b;
-    double v;
-    switch (dtype) {
-      case kU8: v = reinterpret_cast<const uint8_t*>(x)[k]; break;
-      case kI32: v = reinterpret_cast<const int32_t*>(x)[k]; break;
-      case kF32: v = reinterpret_cast<const float*>(x)[k]; break;
-      default: v = reinterpret_cast<const double*>(x)[k]; break;
-    }
-    c += (v < thr) ? 1ull : 0ull;
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
-}
-
 // -------------------------------------------------------------------- launchers
 hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, int ldb, hipStream_t s) {
   const size_t total = (size_t)n * (ldb / 4);
@@ -1768,13 +1748,6 @@ hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s) {
 }
 hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s) {
   hipLaunchKernelGGL(finalize_iters, dim3(1), dim3(64), 0, s, flags, imax, early, dL, user);
-  return hipGetLastError();
-}
-hipError_t launch_count_below(const void* x, int dtype, int64_t rows, int B, int64_t ld, double thr,
-                              unsigned long long* cnt, hipStream_t s) {
-  const int64_t total = rows * (int64_t)B;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
-  hipLaunchKernelGGL(count_below, dim3(grid), dim3(256), 0, s, x, dtype, rows, B, ld, thr, cnt);
   return hipGetLastError();
 }
 

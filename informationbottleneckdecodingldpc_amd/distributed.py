@@ -5,8 +5,8 @@ has no communication backend. Decoding independent codewords partitions perfectl
 multi-GPU design has exactly two exchanges, both off the data path:
 
 * setup: rank 0's code graph (CSR of H) and decoder tables are broadcast once
-  (:func:`broadcast_arrays` — one size broadcast + one packed payload broadcast, over
-  xGMI with the ``nccl``=RCCL backend, or over TCP with ``gloo``);
+  (:func:`broadcast_arrays` — three broadcasts: the header's size, the header, one packed
+  payload; over xGMI with the ``nccl``=RCCL backend, or over TCP with ``gloo``);
 * per Eb/N0 point: one all-reduce of the counters {errors, bits, codewords, iterations}
   (:func:`allreduce_counts`).
 
@@ -71,7 +71,8 @@ def _comm_device() -> torch.device:
 
 
 def broadcast_arrays(arrays: Dict[str, np.ndarray] | None, src: int = 0) -> Dict[str, np.ndarray]:
-    """Broadcast a dict of numpy arrays from ``src`` to every rank (two collectives in total).
+    """Broadcast a dict of numpy arrays from ``src`` to every rank: three broadcasts in total — the header's
+    length, the header (keys, dtypes, shapes, payload size) and one packed uint8 payload.
 
     Non-source ranks pass ``None``. Key order, dtypes and shapes travel in a small header. An initialised
     group of size 1 still runs the collectives (so a 1-GPU ``nccl`` group exercises the device path).

@@ -119,3 +119,51 @@ def test_ber_driver_minsum_llr_input():
                     llr_dtype=torch.float32)
     r = run_ber(dec, cfg)
     assert r.blocks == [1024] and r.errors == [0.0]
+
+
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.int32, torch.float32, torch.float64])
+def test_channel_sample_row_stride(dtype):
+    """ibl_channel_sample with a row stride ld > B (the C ABI's general case; the round-6 kernel's per-block row
+    split): the [n][B] window equals the oracle, the padding columns stay untouched."""
+    from informationbottleneckdecodingldpc_amd import _lib
+    q = _q()
+    n, B, ld = 9, 13, 16
+    buf = torch.full((n, ld), 77, dtype=dtype, device=DEV)
+    cdf = np.ascontiguousarray(q.cdf_t_given_x_equals_zero, np.float64)
+    llr = np.ascontiguousarray(q.output_LLRs, np.float64)
+    _lib.check(_lib.load().ibl_channel_sample(cdf, 16, llr.ctypes.data, 4, 21, n, B, None, buf.data_ptr(),
+                                              engine._DT_ANY[dtype], ld, engine._stream_ptr(buf.device)),
+               "ibl_channel_sample")
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    t = oracle.channel_sample(q.cdf_t_given_x_equals_zero, 4, 21, n, B)
+    want = t if dtype in (torch.uint8, torch.int32) else q.output_LLRs[t].astype(got.dtype)
+    assert np.array_equal(got[:, :B].astype(want.dtype), want)
+    assert np.all(got[:, B:] == 77)
+
+
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.int32, torch.float32, torch.float64])
+@pytest.mark.parametrize("B,ld", [(96, 96), (4096, 4096), (48, 64), (77, 77)])
+def test_counters_vector_and_strided(dtype, B, ld):
+    """ibl_count_below / ibl_count_errors (round 6: one 16-byte word per lane when rows, stride and pointer allow it,
+    else one element; row stride ld >= B) equal numpy on the [rows][B] window."""
+    from informationbottleneckdecodingldpc_amd import _lib
+    rng = np.random.default_rng(B + ld)
+    n, rows = 37, 29
+    full = rng.integers(0, 16, (n, ld)) if dtype in (torch.uint8, torch.int32) else rng.normal(size=(n, ld))
+    bits = rng.integers(0, 2, (n, ld)).astype(np.uint8)
+    thr = 8 if dtype in (torch.uint8, torch.int32) else 0.0
+    x = torch.from_numpy(full).to(dtype).to(DEV)
+    bt = torch.from_numpy(bits).to(DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    L = _lib.load()
+    s = engine._stream_ptr(x.device)
+    _lib.check(L.ibl_count_below(x.data_ptr(), engine._DT_ANY[dtype], rows, B, ld, float(thr), cnt.data_ptr(), s), "cb")
+    assert int(cnt.item()) == int((full[:rows, :B] < thr).sum())
+    _lib.check(L.ibl_count_errors(x.data_ptr(), engine._DT_ANY[dtype], rows, B, ld, float(thr), bt.data_ptr(), ld,
+                                  cnt.data_ptr(), s), "ce")
+    assert int(cnt.item()) == int(((full[:rows, :B] < thr) != (bits[:rows, :B] != 0)).sum())
+    # half thresholds on integer outputs: v < 7.5 <=> v < 8
+    if dtype in (torch.uint8, torch.int32):
+        _lib.check(L.ibl_count_below(x.data_ptr(), engine._DT_ANY[dtype], rows, B, ld, 7.5, cnt.data_ptr(), s), "cb")
+        assert int(cnt.item()) == int((full[:rows, :B] < 7.5).sum())

@@ -4,8 +4,9 @@ Every decoder runs through the BER driver (`ber.run_ber`, the reference's DVB-S2
 with the same seed, batch and block count per point, so each point decodes the identical channel frames (the device
 Philox stream keyed on the global batch index; IB gets the clusters, BP their fp32 LLRs):
 
-  * IB T=16, i_max=50, matching, tables from `tables.de_tables` designed at one Eb/N0 (`--design`, default 0.8 dB:
-    the reference's DVB-S2 configs are designed at one point too, DVB-S2/decoder_config_generation.py:20);
+  * IB T=16, i_max=50, matching, tables from `tables.de_tables` designed at one Eb/N0 per curve (`--designs`,
+    default 0.75 and 0.8 dB: the reference's DVB-S2 configs are designed at one point too,
+    DVB-S2/decoder_config_generation.py:20);
   * IB T=16 with the round-5 fixed-alphabet `llr_tables` (designed per point) for comparison;
   * BP fp32 (BeliefPropagationDecoderClassIrregular) at i_max 50 and 100.
 
@@ -27,7 +28,7 @@ def main():
     p.add_argument("--points", default="0.8:1.3:0.05")
     p.add_argument("--batches", type=int, default=4)
     p.add_argument("--batch", type=int, default=8192)
-    p.add_argument("--design", type=float, default=0.8)
+    p.add_argument("--designs", default="0.75,0.8", help="design Eb/N0 of the DE tables, one IB curve each")
     p.add_argument("--decoders", default="ib_de,ib_llr,bp50,bp100")
     a = p.parse_args()
     import torch
@@ -43,15 +44,21 @@ def main():
     rho, lam = tables.edge_degree_distributions(g)
     B = a.batch
     t0 = time.time()
-    qd = UniformQuantizer(sigma2_from_ebn0(a.design, g.R_c), 16)
-    de = tables.de_tables(qd.p_t_given_x0, qd.output_LLRs, rho, lam, 50)
-    design_s = time.time() - t0
+    designs = [float(x) for x in a.designs.split(",")]
+    des = {}
+    for dz in designs:
+        qd = UniformQuantizer(sigma2_from_ebn0(dz, g.R_c), 16)
+        des[f"ib_de{dz:g}"] = tables.de_tables(qd.p_t_given_x0, qd.output_LLRs, rho, lam, 50)
+    design_s = (time.time() - t0) / len(designs)
+    names = []
+    for n in a.decoders.split(","):
+        names += list(des) if n == "ib_de" else [n]
     curves = {}
-    for name in a.decoders.split(","):
+    for name in names:
         ber, errs, secs = [], [], []
         for x in pts:
-            if name == "ib_de":
-                tb = de
+            if name in des:
+                tb = des[name]
             elif name == "ib_llr":
                 q = UniformQuantizer(sigma2_from_ebn0(x, g.R_c), 16)
                 tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 50)
@@ -84,7 +91,7 @@ def main():
                       "channel": "BPSK/AWGN, 16-cluster uniform quantiser (AD_max_abs 3), all-zero codeword, Philox seed 7",
                       "batch": B, "blocks_per_point": a.batches * B, "bits_per_point": a.batches * B * int(g.data_len),
                       "early_stop": "batch-global (never triggers at this batch: the degree-1 parity variable)",
-                      "ib_design_ebn0_db": a.design, "de_design_seconds": round(design_s, 2),
+                      "ib_design_ebn0_db": designs, "de_design_seconds_each": round(design_s, 2),
                       "ebn0_db": pts, "curves": curves, "summary": summary}), flush=True)
 
 
