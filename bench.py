@@ -64,7 +64,7 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--early-stop", action="store_true",
                    help="batch-global early stop on (SURVEY §8(d)'s second line: at 1.0 dB unless --ebn0 is given); "
-                        "IB decoders use LLR-derived tables (tables.llr_tables) so the batch can converge")
+                        "IB decoders use density-evolution tables (tables.de_tables, designed at 0.75 dB) so the batch can converge")
     p.add_argument("--sub-batch", type=int, default=0,
                    help="IB only: decode the batch as sequential sub-batches of this many codewords (one decoder sized "
                         "for the sub-batch: its working set can stay in the 256-MiB Infinity Cache across passes)")
@@ -487,11 +487,15 @@ def build_decoder(a, G, g, arrays, q, B):
     import torch
 
     from informationbottleneckdecodingldpc_amd import engine, tables
+    from informationbottleneckdecodingldpc_amd.channel import UniformQuantizer, sigma2_from_ebn0
     I, match = a.imax, not a.no_match
     if a.kind == "ib":
         if a.early_stop:
-            # LLR-derived tables (an approximate BP in the T=16 alphabet) so the batch can converge and stop
-            tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, I)
+            # tables that decode (so the batch can converge and stop): discrete density evolution at 0.75 dB, the
+            # design point of the DVB-S2 curves in profiles/r06_dvbs2_ber_curves.json (round 6; was llr_tables)
+            qd = UniformQuantizer(sigma2_from_ebn0(0.75, g.R_c), 16)
+            rho, lam = tables.edge_degree_distributions(g)
+            tb = tables.de_tables(qd.p_t_given_x0, qd.output_LLRs, rho, lam, I)
             match = True
         else:
             tb = tables.IBTables(16, 16, g.d_c_max, g.d_v_max, I, arrays["cn"], arrays["vn"], arrays["mc"], arrays["mv"])
@@ -644,7 +648,7 @@ def main():
             "dtype": dtype,
             "data": f"synthetic: all-zero codeword, BPSK/AWGN at Eb/N0 {a.ebn0} dB quantised to 16 clusters "
                     f"(device Philox, key {CH_SEED}, global batch {a.batch_offset}+rank); "
-                    f"{('LLR-derived T=16 IB tables' if early else 'random T=16 IB tables') if a.kind == 'ib' else 'cluster LLRs'}"
+                    f"{('DE-designed T=16 IB tables (0.75 dB)' if early else 'random T=16 IB tables') if a.kind == 'ib' else 'cluster LLRs'}"
                     f"; {code_desc}",
             "config": {"workload": f"{code_name}, "
                                    f"{'IB-LUT T=16' if a.kind == 'ib' else a.kind + ' fp32'}, i_max={I}, "

@@ -27,6 +27,7 @@
 //     into the check-node pass (parity of its inputs), and published as device flags that
 //     gate the next launches — no host readback inside the iteration loop.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -623,6 +624,66 @@ __device__ __forceinline__ void ib_phase(const IbFastArgs& a, uint32_t lane4, ui
   if (trace_items && lane == 0) *trace_items += (uint64_t)done;
 }
 
+// Variable pass, interleaved heavy / light items (IBL_VN_MIX3): every wave runs one heavy item
+// (degree > kLightD: LDS-lookup-bound) and two light items (HBM-bound) in turn, so each SIMD always holds both
+// kinds. Three buffers in rotation (one heavy, two light — DVB-S2 has 2 light items per heavy one: 51,840 light
+// nodes x 4 chunks of 2048 codewords against 12,960 heavy nodes x 8 chunks of 1024): the item computed next is
+// always the oldest in flight, so its wait leaves the other two buffers' loads outstanding. When one stream runs
+// out the wave computes the buffers it holds and finishes the other stream with the ping-pong phase.
+#ifndef IBL_VN_MIX3
+#define IBL_VN_MIX3 0
+#endif
+template <class BufH, class BufL>
+__device__ __forceinline__ void ib_phase_mix3(const IbFastArgs& a, uint32_t lane4, uint32_t lane8c, int lane, int hend,
+                                              int lend, int nw, int wpb, int* ctr, uint64_t* trace_items,
+                                              const PhaseItems pih, const PhaseItems pil) {
+  auto compute = [&](const auto& cur) __attribute__((always_inline)) {
+    using B = std::decay_t<decltype(cur)>;
+    settle<true>(cur);
+    switch (cur.d) {
+      case 1: if constexpr (B::kMax == kLightD) vn_compute<1>(a, lane4, lane8c, cur, 0); break;
+#define X(D) case D: if constexpr (D <= B::kMax && (B::kMax == kLightD || D > kLightD)) vn_compute<D>(a, lane4, lane8c, cur, a.fslot[D]); break;
+      IBL_DEG_CASES(X)
+#undef X
+      default: break;
+    }
+  };
+  const int hbase = (int)blockIdx.x * wpb, lbase = hend + (int)blockIdx.x * wpb;
+  auto hitem = [&](int k) { return hbase + (k % wpb) + nw * (k / wpb); };
+  auto litem = [&](int k) { return lbase + (k % wpb) + nw * (k / wpb); };
+  BufH h;
+  BufL l1, l2;
+  int ih = hitem(take_ticket(ctr, lane));
+  fetch_item<BufH, true, false>(a, min(ih, hend - 1), lane, h, pih);
+  int i1 = litem(take_ticket(ctr + 1, lane));
+  fetch_item<BufL, true, false>(a, min(i1, lend - 1), lane, l1, pil);
+  int i2 = litem(take_ticket(ctr + 1, lane));
+  fetch_item<BufL, true, false>(a, min(i2, lend - 1), lane, l2, pil);
+  int done = 0;
+  for (;;) {
+    if (ih >= hend || i1 >= lend || i2 >= lend) break;
+    compute(h);
+    ih = hitem(take_ticket(ctr, lane));
+    fetch_item<BufH, true, false>(a, min(ih, hend - 1), lane, h, pih);
+    compute(l1);
+    i1 = litem(take_ticket(ctr + 1, lane));
+    fetch_item<BufL, true, false>(a, min(i1, lend - 1), lane, l1, pil);
+    compute(l2);
+    i2 = litem(take_ticket(ctr + 1, lane));
+    fetch_item<BufL, true, false>(a, min(i2, lend - 1), lane, l2, pil);
+    done += 3;
+  }
+  // the valid items still held, then whatever is left of either stream
+  if (ih < hend) { compute(h); ++done; }
+  if (i1 < lend) { compute(l1); ++done; }
+  if (i2 < lend) { compute(l2); ++done; }
+  if (trace_items && lane == 0) *trace_items += (uint64_t)done;
+  bool unsat = false;
+  ib_phase<BufH, true, false, kLightD, 2>(a, lane4, lane8c, lane, 0, hend, nw, wpb, ctr, false, unsat, trace_items, pih);
+  ib_phase<BufL, true, false, 0, (IBL_LIGHT_DEPTH)>(a, lane4, lane8c, lane, hend, lend, nw, wpb, ctr + 1, false, unsat,
+                                                   trace_items, pil);
+}
+
 template <int MAXD, bool VN, bool GATHER>
 __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds) {
   const int lane = threadIdx.x & 63;
@@ -657,6 +718,15 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
 #define IBL_MIX16 4
 #endif
   const bool light_first = VN && (int)(threadIdx.x >> 6) * 16 < wpb * IBL_MIX16;
+  if constexpr (VN && MAXD <= 8 && IBL_VN_MIX3) {
+    if (a.n_heavy > 0 && a.n_heavy < a.n_nodes) {
+      ib_phase_mix3<ItemBuf<MAXD, W>, ItemBuf<kLightD, LW>>(a, lane4, lane8c, lane, heavy_end, nitems, nw, wpb, ctr,
+                                                            trace_items, PhaseItems{0, 0, a.nchunks},
+                                                            PhaseItems{heavy_end, a.n_heavy, nch_l});
+      if (a.trace && lane == 0) a.trace[3 * gw + 1] = __builtin_readcyclecounter();
+      return;
+    }
+  }
 #pragma unroll 1
   for (int r = 0; r < 2; ++r) {
     if ((r == 0) != light_first)

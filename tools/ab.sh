@@ -3,7 +3,7 @@
 set -u
 TAG=$1; VARS=$2; shift 2
 O=gpurun_out/$TAG; mkdir -p $O
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in $VARS; do
     if [ $v = base ]; then LIBV=""; else LIBV=$PWD/informationbottleneckdecodingldpc_amd/variants/libibldpc_$v.so; fi
     IBLDPC_LIB=$LIBV timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/ab_${v}_$rep.json 2> $O/ab_${v}_$rep.err

@@ -35,12 +35,13 @@ def run(case, batches, B):
     if case.startswith("c4"):
         from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
             Discrete_LDPC_Decoder_class_irregular
-        q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
-        tb = tables.llr_tables(q.output_LLRs, g.d_c_max, g.d_v_max, 50)
+        q = UniformQuantizer(sigma2_from_ebn0(0.75, g.R_c), 16)      # DE tables designed at 0.75 dB (round 6)
+        rho, lam = tables.edge_degree_distributions(g)
+        tb = tables.de_tables(q.p_t_given_x0, q.output_LLRs, rho, lam, 50)
         dec = Discrete_LDPC_Decoder_class_irregular(H, 50, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
                                                     match="true")
         cfg["encoded"] = case == "c4enc"
-        what = "IB T=16 i_max=50 (LLR-derived tables), Discrete_LDPC_Decoder_class_irregular"
+        what = "IB T=16 i_max=50 (DE tables designed at 0.75 dB), Discrete_LDPC_Decoder_class_irregular"
     else:
         from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
         dec = BeliefPropagationDecoderClassIrregular(H, 100, 16, B)

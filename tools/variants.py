@@ -24,6 +24,8 @@ VARIANTS = {
     # variable pass co-scheduling: waves with (threadIdx.x >> 8) < IBL_MIX take the light (degree <= 4,
     # HBM-bound) items first, the others the heavy (LDS-bound) ones
     "mix1": ["IBL_MIX16=4"],
+    # round 6: every wave interleaves one heavy and two light variable items (ib_phase_mix3)
+    "vmix3": ["IBL_VN_MIX3=1"],
     "mix2": ["IBL_MIX16=8"],
     "mix3": ["IBL_MIX16=12"],
     "mixw2": ["IBL_MIX16=2"],
