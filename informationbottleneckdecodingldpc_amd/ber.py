@@ -64,6 +64,7 @@ class BERConfig:
     llr_dtype: Optional[object] = None    # float decoders: torch dtype of the channel LLRs
     encoded: bool = False                 # random encoded codewords (LDPC_BPSK_Transmitter) instead of all-zero
     pipeline: bool = True                 # device double buffering + side-stream counts (see the module docstring)
+    gen_chunk: int = 1 << 22              # pipelined channel: samples per side-stream launch (0 = one launch a batch)
 
 
 @dataclass
@@ -190,6 +191,7 @@ class _DeviceRunner:
         self.torch = torch
         self.decoder, self.kind, self.quanti, self.tx = decoder, kind, quanti, tx
         self.B, self.pb_ch, self.pb_bits, self.err_rows, self.thr = B, pb_ch, pb_bits, err_rows, thr
+        self.gen_chunk = int(cfg.gen_chunk)
         dev = decoder.device
         self.dev = dev
         self.main = torch.cuda.current_stream(dev)
@@ -217,8 +219,18 @@ class _DeviceRunner:
                 random_bits(self.info[slot], self.tx.seed, g * self.pb_bits)
                 self.tx.encoder.encode_batch(self.info[slot], self.code[slot])
                 bits = self.code[slot]
-            channel_sample(self.ch[slot], q.cdf_t_given_x_equals_zero, q.seed, g * self.pb_ch,
-                           llr=None if self.kind == "ib" else q.output_LLRs, bits=bits)
+            # in row slices of ~gen_chunk samples: each slice is a short launch that can take the CUs in the gaps
+            # between the decode's per-pass launches instead of holding the chip for the whole batch's sampling.
+            # Slice rows start at multiples of 4, so every slice begins on a Philox block (4 samples): slice
+            # [r0, r1) is the batch's stream from element r0 * B on, at counter g * pb_ch + r0 * B / 4.
+            out = self.ch[slot]
+            n, B = out.shape
+            rows = n if self.gen_chunk <= 0 else max(4, (self.gen_chunk // max(B, 1)) // 4 * 4)
+            llr = None if self.kind == "ib" else q.output_LLRs
+            for r0 in range(0, n, rows):
+                r1 = min(n, r0 + rows)
+                channel_sample(out[r0:r1], q.cdf_t_given_x_equals_zero, q.seed, g * self.pb_ch + (r0 * B) // 4,
+                               llr=llr, bits=None if bits is None else bits[r0:r1])
             ev = torch.cuda.Event()
             ev.record(self.side)
         self.ready[slot], self.slot_g[slot] = ev, g

@@ -1501,28 +1501,61 @@ __global__ void ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8, 
 }
 
 // ------------------------------------------- channel staging for the fast path (-> 4-bit nibbles)
-__global__ void ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes) {
-  const int words = min(ldb_bytes >> 2, (B + 7) >> 3);   // padding words of a row are never output
-  const size_t total = (size_t)n * words;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int row = (int)(i / words);
-    const int cw0 = (int)(i - (size_t)row * words) * 8;
-    uint32_t packed = 0;
+// Channel staging of the fast path: cluster ids (u8 / i32, [N][B]) -> 4-bit nibbles [N][ldb bytes], the first
+// ceil(B / 8) words of every row (the rest of a row is padding no output reads). A block takes one (row, 1024-word
+// segment) item at a time: one scalar division per item instead of one 64-bit division per output word (round 6:
+// 0.39 -> ~0.1 ms at C4's batch), and rows whose length and base allow it are read as 8 / 32-byte vectors.
+__device__ __forceinline__ uint32_t nib8(const uint32_t (&v)[8]) {
+  uint32_t p = 0;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int cw = cw0 + s;
-      uint32_t v = 0;
-      if (cw < B) {
-        if (dtype == kU8) {
-          v = reinterpret_cast<const uint8_t*>(ch)[(size_t)row * B + cw];
+  for (int s = 0; s < 8; ++s) p |= min(v[s], 15u) << (4 * s);
+  return p;
+}
+template <int DT>
+__global__ __launch_bounds__(256) void ib_stage4(const void* ch, int n, int B, uint8_t* ch4, int ldb_bytes, int words,
+                                                 int64_t nseg, int vec) {
+  constexpr int U = 4;   // words per lane and item
+  const int64_t items = (int64_t)n * nseg;
+  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+    const int row = (int)(it / nseg);
+    const int w0 = (int)(it - (int64_t)row * nseg) * (256 * U) + (int)threadIdx.x;
+    uint32_t v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int w = w0 + 256 * u, cw0 = 8 * w;
+      if (vec && w < words) {   // B % 8 == 0 and an aligned base: the word's 8 codewords are in the row
+        if constexpr (DT == kU8) {
+          const uint2 q = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(ch) + (size_t)row * B + cw0);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            v[u][s] = (q.x >> (8 * s)) & 0xffu;
+            v[u][4 + s] = (q.y >> (8 * s)) & 0xffu;
+          }
         } else {
-          const int32_t x = reinterpret_cast<const int32_t*>(ch)[(size_t)row * B + cw];
-          v = (uint32_t)min(max(x, 0), 255);
+          const int4* p = reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(ch) + (size_t)row * B + cw0);
+          const int4 q0 = p[0], q1 = p[1];
+          const int32_t x[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+          for (int s = 0; s < 8; ++s) v[u][s] = (uint32_t)min(max(x[s], 0), 255);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int cw = cw0 + s;
+          uint32_t e = 0;
+          if (w < words && cw < B) {
+            if constexpr (DT == kU8) e = reinterpret_cast<const uint8_t*>(ch)[(size_t)row * B + cw];
+            else e = (uint32_t)min(max(reinterpret_cast<const int32_t*>(ch)[(size_t)row * B + cw], 0), 255);
+          }
+          v[u][s] = e;
         }
       }
-      packed |= min(v, 15u) << (4 * s);
     }
-    *reinterpret_cast<uint32_t*>(ch4 + (size_t)row * ldb_bytes + cw0 / 2) = packed;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int w = w0 + 256 * u;
+      if (w < words) *reinterpret_cast<uint32_t*>(ch4 + (size_t)row * ldb_bytes + 4 * (size_t)w) = nib8(v[u]);
+    }
   }
 }
 
@@ -1652,9 +1685,15 @@ hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8
   return hipGetLastError();
 }
 hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s) {
-  const size_t total = (size_t)n * std::min(ldb_bytes / 4, (B + 7) / 8);
-  const int grid = (int)std::min<size_t>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(ib_stage4, dim3(grid), dim3(256), 0, s, ch, dtype, n, B, ch4, ldb_bytes);
+  const int words = std::min(ldb_bytes / 4, (B + 7) / 8);
+  const int64_t nseg = (words + 1023) / 1024, items = (int64_t)n * nseg;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
+  const size_t align = dtype == kU8 ? 8 : 16;
+  const int vec = (B % 8) == 0 && (reinterpret_cast<uintptr_t>(ch) % align) == 0;
+  if (dtype == kU8)
+    hipLaunchKernelGGL(ib_stage4<kU8>, dim3(grid), dim3(256), 0, s, ch, n, B, ch4, ldb_bytes, words, nseg, vec);
+  else
+    hipLaunchKernelGGL(ib_stage4<kI32>, dim3(grid), dim3(256), 0, s, ch, n, B, ch4, ldb_bytes, words, nseg, vec);
   return hipGetLastError();
 }
 hipError_t launch_ib_cn_fast(const IbFastArgs& a, int maxd, int grid, int block, size_t lds, hipStream_t s) {
