@@ -272,6 +272,30 @@ int ibl_random_bits(uint64_t seed, uint64_t offset, int32_t n, int32_t B, uint8_
 int ibl_count_errors(const void* d_x, int32_t dtype, int64_t rows, int32_t B, int64_t ld, double threshold,
                      const uint8_t* d_bits, int64_t bits_ld, int64_t* d_count, void* stream);
 
+/* ---- Multi-GPU batch split without torch ------------------------------------------
+ * The protocol of informationbottleneckdecodingldpc_amd/distributed.py for C / C++ callers: one process per
+ * GPU; rank 0 builds H and the tables and broadcasts them once (ibl_comm_broadcast of the sizes, then of
+ * each array — H's CSR and the LUT / matching vectors of ibl_ib_create); every rank decodes its contiguous
+ * codeword range (ibl_shard_range) with its own ibl_graph / decoder; per Eb/N0 point one
+ * ibl_comm_allreduce_sum_i64 of the counters {errors, bits, codewords}. No collective inside a decode (the
+ * reference decodes on one OpenCL device and has no communication, discrete_LDPC_decoder_irreg.py:174-175).
+ * Collectives run on RCCL (NCCL's API on ROCm, over xGMI), loaded at run time (dlopen librccl.so.1);
+ * IBL_EUNSUPPORTED when it cannot be loaded.
+ */
+/* [start, start + count) of `rank`'s share of `total` codewords (contiguous, sizes differ by at most 1). */
+int ibl_shard_range(int64_t total, int32_t rank, int32_t world, int64_t* start, int64_t* count);
+#define IBL_COMM_ID_BYTES 128
+typedef struct ibl_comm ibl_comm;
+/* rank 0 creates the id (IBL_COMM_ID_BYTES bytes) and hands it to every rank out of band (MPI, a file, TCP) */
+int ibl_comm_unique_id(uint8_t* id);
+/* collective: every rank of `nranks` calls it with the same id, its rank and its device */
+int ibl_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, ibl_comm** out);
+/* d_buf: device memory of `bytes` bytes on the communicator's device; asynchronous on `stream` */
+int ibl_comm_broadcast(ibl_comm* c, void* d_buf, int64_t bytes, int32_t root, void* stream);
+/* in-place sum over ranks of `count` int64 device values; asynchronous on `stream` */
+int ibl_comm_allreduce_sum_i64(ibl_comm* c, int64_t* d_buf, int64_t count, void* stream);
+void ibl_comm_destroy(ibl_comm* c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libibldpc.so")
-SOURCES = ["ib_kernels.hip", "float_kernels.hip", "channel_kernels.hip", "encoder_kernels.hip", "capi.hip"]
+SOURCES = ["ib_kernels.hip", "float_kernels.hip", "channel_kernels.hip", "encoder_kernels.hip", "capi.hip", "comm.hip"]
 ARCH = os.environ.get("IBLDPC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
@@ -57,7 +57,7 @@ def build(force: bool = False, verbose: bool = False, defines=(), lib: str = LIB
                     sys.stderr.write(r.stderr)
     objs = [os.path.join(objdir, s.replace(".hip", ".o")) for s in SOURCES]
     if force or jobs or _stale(lib, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-ldl", "-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             sys.stderr.write(r.stdout + r.stderr)

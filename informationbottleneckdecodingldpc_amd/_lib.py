@@ -40,7 +40,10 @@ EXPORTS = [
     "ibl_encoder_destroy",
     "ibl_random_bits",
     "ibl_count_errors",
+    "ibl_shard_range", "ibl_comm_unique_id", "ibl_comm_create", "ibl_comm_broadcast", "ibl_comm_allreduce_sum_i64",
+    "ibl_comm_destroy",
 ]
+IBL_COMM_ID_BYTES = 128
 
 
 class IBLError(RuntimeError):
@@ -109,6 +112,13 @@ def load():
     L.ibl_encoder_destroy.restype = None
     L.ibl_random_bits.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _i32, _i32, _vp, _vp]
     L.ibl_count_errors.argtypes = [_vp, _i32, _i64, _i32, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
+    L.ibl_shard_range.argtypes = [_i64, _i32, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
+    L.ibl_comm_unique_id.argtypes = [_vp]
+    L.ibl_comm_create.argtypes = [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)]
+    L.ibl_comm_broadcast.argtypes = [_vp, _vp, _i64, _i32, _vp]
+    L.ibl_comm_allreduce_sum_i64.argtypes = [_vp, _vp, _i64, _vp]
+    L.ibl_comm_destroy.argtypes = [_vp]
+    L.ibl_comm_destroy.restype = None
     for name in EXPORTS:
         getattr(L, name)
     _lib = L
@@ -141,3 +151,10 @@ def map_node_connections(n_v: int, n_c: int, indptr: np.ndarray, cols: np.ndarra
     tv = np.zeros(E, np.int32)
     check(L.ibl_map_node_connections(n_v, n_c, indptr, cols, cs, cd, tc, vs, vd, tv), "ibl_map_node_connections")
     return dict(cn_start=cs, cn_deg=cd, tgt_cn=tc, vn_start=vs, vn_deg=vd, tgt_vn=tv)
+
+
+def shard_range(total: int, rank: int, world: int):
+    """(start, count) of rank's contiguous share of `total` codewords (``ibl_shard_range``; host only)."""
+    a, b = _i64(0), _i64(0)
+    check(load().ibl_shard_range(int(total), int(rank), int(world), ctypes.byref(a), ctypes.byref(b)), "ibl_shard_range")
+    return int(a.value), int(b.value)

@@ -38,6 +38,7 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int ibl::set_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
 // Diagnostic builds: IBL_DEBUG_SYNC=1 synchronises after every launch so an asynchronous fault is
 // reported at the launch that caused it (breaks the no-host-sync property of decode).
 static bool debug_sync() {

@@ -67,6 +67,9 @@ constexpr int kLdsBytes = 160 * 1024;
 
 enum Dtype : int32_t { kU8 = 1, kI32 = 2, kF32 = 3, kF64 = 4 };
 
+// the C ABI's per-thread last error (capi.hip; ibl_last_error): other translation units report through it
+int set_error(int code, const char* msg);
+
 // Read-only graph arrays read through the constant address space: uniform indices become scalar
 // loads (the compiler cannot otherwise prove they do not alias the inbox being written, and would
 // issue vector loads whose waits drain every outstanding row load).

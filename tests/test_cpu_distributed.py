@@ -118,3 +118,16 @@ def test_shard_range_partitions(total, world):
         assert s == pos
         pos += c
     assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+@pytest.mark.parametrize("total,world", [(0, 1), (7, 3), (8192, 8), (65536, 8), (100, 7), (5, 8)])
+def test_c_abi_shard_range_equals_python(total, world):
+    """ibl_shard_range (the batch split for callers without torch, include/ibldpc.h) equals distributed.shard_range:
+    contiguous ranges that tile [0, total) with sizes differing by at most one."""
+    from informationbottleneckdecodingldpc_amd import _lib
+    from informationbottleneckdecodingldpc_amd.distributed import shard_range
+    got = [_lib.shard_range(total, r, world) for r in range(world)]
+    assert got == [shard_range(total, r, world) for r in range(world)]
+    assert sum(c for _, c in got) == total and all(got[r][0] + got[r][1] == got[r + 1][0] for r in range(world - 1))
+    with pytest.raises(_lib.IBLError):
+        _lib.shard_range(total, world, world)

@@ -84,3 +84,31 @@ def test_rccl_group_collectives_and_ber_exchange():
     assert res["errors"] == [float(e) for e in r.errors] and res["blocks"] == list(r.blocks)
     assert len(res["ebn0"]) == 2
     torch.cuda.synchronize()
+
+
+def test_c_abi_communicator_size_one():
+    """The C ABI's RCCL communicator (ibl_comm_*: for callers without torch.distributed) as a 1-rank group on the
+    box's GPU: the setup broadcast leaves the root's bytes in place, the counter all-reduce sums over one rank."""
+    import ctypes
+
+    import torch
+    from informationbottleneckdecodingldpc_amd import _lib
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * _lib.IBL_COMM_ID_BYTES)()
+    _lib.check(L.ibl_comm_unique_id(uid), "ibl_comm_unique_id")
+    comm = ctypes.c_void_p()
+    _lib.check(L.ibl_comm_create(uid, 1, 0, 0, ctypes.byref(comm)), "ibl_comm_create")
+    try:
+        s = torch.cuda.current_stream().cuda_stream
+        buf = torch.arange(1000, dtype=torch.uint8, device="cuda:0")
+        want = buf.clone()
+        _lib.check(L.ibl_comm_broadcast(comm, buf.data_ptr(), buf.numel(), 0, s), "ibl_comm_broadcast")
+        cnt = torch.tensor([5, -3, 2 ** 40], dtype=torch.int64, device="cuda:0")
+        _lib.check(L.ibl_comm_allreduce_sum_i64(comm, cnt.data_ptr(), 3, s), "ibl_comm_allreduce_sum_i64")
+        torch.cuda.synchronize()
+        assert torch.equal(buf, want)
+        assert cnt.cpu().tolist() == [5, -3, 2 ** 40]
+        with pytest.raises(_lib.IBLError):
+            _lib.check(L.ibl_comm_broadcast(comm, buf.data_ptr(), 10, 1, s), "ibl_comm_broadcast")   # root >= nranks
+    finally:
+        L.ibl_comm_destroy(comm)
