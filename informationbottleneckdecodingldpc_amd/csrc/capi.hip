@@ -713,8 +713,11 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     return IBL_OK;
   }
   if (h->fast && B <= h->small_b) {
-    // small batch: (task, word) items, lane = node (ib_*_small); the pass schedule of the fast path
-    const int ldbb = h->ldb / 2, nwords = (B + 7) / 8;
+    // small batch: (task, word) items, lane = node (ib_*_small); the pass schedule of the fast path.
+    // Rows are packed to the batch's words (4 * nwords bytes, not the per-pass path's ldb / 2): a pass
+    // then touches E * 4 * nwords bytes of each inbox (B = 2 on DVB-S2: 0.9 MB, resident in the L2s and
+    // the MALL) instead of one 128-B line per edge (29 MB)
+    const int nwords = (B + 7) / 8, ldbb = 4 * nwords;
     HIPCHK(launch_ib_stage4(d_ch, ch_dtype, g->n_v, B, h->ch8, ldbb, s));
     auto grid_of = [&](int ntask, size_t lds) {
       const int per_cu = std::max(1, (int)(kLdsBytes / std::max<size_t>(lds, 1)));
@@ -1227,17 +1230,19 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     }
     return IBL_OK;
   }
-  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, rule, h->bad, s));
   if (B <= h->small_b) {
-    // small batch: (task, word) items, lane = node (fl_*_small); the per-pass schedule without the fold
-    const int nwords = (B + cwl - 1) / cwl;
+    // small batch: (task, word) items, lane = node (fl_*_small); the per-pass schedule without the fold.
+    // Rows packed to the batch (B rounded up to 4 codewords: fl_send's quads, 16-byte pieces) instead of
+    // the per-pass path's ldb, so a pass touches E x ldbs elements of each inbox, not one line per edge
+    const int nwords = (B + cwl - 1) / cwl, ldbs = (B + 3) / 4 * 4;
+    HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, ldbs, rule, h->bad, s));
     auto grid_of = [&](int ntask) {
       const int need = (ntask * nwords + kFlSmallBlock / 64 - 1) / (kFlSmallBlock / 64);
       return std::max(1, std::min(need, 4 * g->num_cus));
     };
     FlArgs send{};
     send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
-    send.n_nodes = g->n_v; send.ldb = h->ldb; send.B = B;
+    send.n_nodes = g->n_v; send.ldb = ldbs; send.B = B;
     HIPCHK(launch_fl_send(send, h->prec, s));
     FlArgs cn{}, vn{};
     cn.in = h->cin; cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.ch = h->chf;
@@ -1247,7 +1252,7 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     cn.llr_max = vn.llr_max = h->llr_max;
     cn.n_nodes = g->n_c; vn.n_nodes = g->n_v;
     cn.nwords = vn.nwords = nwords;
-    cn.ldb = vn.ldb = h->ldb;
+    cn.ldb = vn.ldb = ldbs;
     cn.B = vn.B = B;
     const int gcn = grid_of(g->n_cn_task), gvn = grid_of(g->n_vn_task);
     for (int j = 1; j < I; ++j) {
@@ -1264,11 +1269,12 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     FlDecArgs dc{};
     dc.vin0 = h->vbuf0; dc.vin1 = h->vbuf1; dc.ch = h->chf; dc.start = g->vn_start; dc.deg = g->vn_deg;
-    dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.n_nodes = g->n_v; dc.ldb = h->ldb; dc.B = B;
+    dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype; dc.n_nodes = g->n_v; dc.ldb = ldbs; dc.B = B;
     dc.info = g->vn_info; dc.task = g->vn_task; dc.n_tasks = g->n_vn_task; dc.nwords = nwords;
     HIPCHK(launch_fl_dec_small(dc, h->prec, grid_of(g->n_vn_task), s));
     return IBL_OK;
   }
+  HIPCHK(launch_fl_stage(d_llr, llr_dtype, g->n_v, B, h->chf, h->prec, h->ldb, rule, h->bad, s));
   FlArgs send{};
   send.ch = h->chf; send.out = h->cin;   // = cb[1] below
   send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;

@@ -21,14 +21,16 @@ namespace {
 
 int comm_fail(int code, const std::string& msg) { return ibl::set_error(code, msg.c_str()); }
 
+// entry points typed from rccl.h's own declarations (a hand-written signature that drifts from the
+// library's is an ABI mismatch no compiler sees through dlsym)
 struct Rccl {
   void* so = nullptr;
-  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
-  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
-  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
-  ncclResult_t (*bcast)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
-  ncclResult_t (*allreduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
-  const char* (*errstr)(ncclResult_t) = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclBroadcast) bcast = nullptr;   // (sendbuff, recvbuff, count, type, root, comm, stream)
+  decltype(&ncclAllReduce) allreduce = nullptr;
+  decltype(&ncclGetErrorString) errstr = nullptr;
 };
 
 const Rccl* rccl(std::string* err) {
@@ -126,7 +128,7 @@ int ibl_comm_broadcast(ibl_comm* c, void* d_buf, int64_t bytes, int32_t root, vo
   if (!c || (!d_buf && bytes > 0) || bytes < 0 || root < 0 || root >= c->nranks)
     return comm_fail(IBL_EINVAL, "bad broadcast arguments");
   if (hipSetDevice(c->device) != hipSuccess) return comm_fail(IBL_EHIP, "hipSetDevice failed");
-  NCCLCHK(c->r, c->r->bcast(d_buf, (size_t)bytes, ncclUint8, root, c->comm, (hipStream_t)stream));
+  NCCLCHK(c->r, c->r->bcast(d_buf, d_buf, (size_t)bytes, ncclUint8, root, c->comm, (hipStream_t)stream));
   return IBL_OK;
 }
 

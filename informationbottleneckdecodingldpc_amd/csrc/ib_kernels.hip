@@ -1559,6 +1559,29 @@ __global__ __launch_bounds__(256) void ib_stage4(const void* ch, int n, int B, u
   }
 }
 
+// Small batches (rows of a few words, packed: ldb_bytes = 4 * words): one thread per (row, word), so a block's
+// 256 threads write 1 KiB of consecutive staged words instead of one block per row with one busy lane.
+template <int DT>
+__global__ __launch_bounds__(256) void ib_stage4_words(const void* ch, int n, int B, uint8_t* ch4, int ldb_bytes,
+                                                       int words) {
+  const int total = n * words;
+  for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int row = i / words, w = i - row * words;
+    uint32_t v[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int cw = 8 * w + s;
+      uint32_t e = 0;
+      if (cw < B) {
+        if constexpr (DT == kU8) e = reinterpret_cast<const uint8_t*>(ch)[(size_t)row * B + cw];
+        else e = (uint32_t)min(max(reinterpret_cast<const int32_t*>(ch)[(size_t)row * B + cw], 0), 255);
+      }
+      v[s] = e;
+    }
+    *reinterpret_cast<uint32_t*>(ch4 + (size_t)row * ldb_bytes + 4 * (size_t)w) = nib8(v);
+  }
+}
+
 // ----------------------------------------------------------------- generic IB path
 // One thread per (node, codeword); reference-exact flat LUT indexing (index clamped to the
 // vector so malformed input cannot fault). Used when T_ch != T_dec, T_dec > 16 or a node
@@ -1686,6 +1709,14 @@ hipError_t launch_ib_stage(const void* ch, int dtype, int n, int B, uint8_t* ch8
 }
 hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch4, int ldb_bytes, hipStream_t s) {
   const int words = std::min(ldb_bytes / 4, (B + 7) / 8);
+  if (words <= 32 && (int64_t)n * words < (1ll << 31)) {   // small batches: one thread per (row, word)
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(((int64_t)n * words + 255) / 256, 8192));
+    if (dtype == kU8)
+      hipLaunchKernelGGL(ib_stage4_words<kU8>, dim3(grid), dim3(256), 0, s, ch, n, B, ch4, ldb_bytes, words);
+    else
+      hipLaunchKernelGGL(ib_stage4_words<kI32>, dim3(grid), dim3(256), 0, s, ch, n, B, ch4, ldb_bytes, words);
+    return hipGetLastError();
+  }
   const int64_t nseg = (words + 1023) / 1024, items = (int64_t)n * nseg;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
   const size_t align = dtype == kU8 ? 8 : 16;
