@@ -62,6 +62,8 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=int, default=100000, help="cap on the CPU-baseline sample (sized to ~12 s of CPU work)")
     p.add_argument("--cpu-procs", type=int, default=0, help="CPU-baseline processes / oracle threads (0 = this job's CPU share, bench.cpu_share())")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-kernel-events", action="store_true",
+                   help="diagnostics: no HIP events around the launches (value without their gaps; no roofline timing)")
     p.add_argument("--early-stop", action="store_true",
                    help="batch-global early stop on (SURVEY §8(d)'s second line: at 1.0 dB unless --ebn0 is given); "
                         "IB decoders use density-evolution tables (tables.de_tables, designed at 0.75 dB) so the batch can converge")
@@ -151,7 +153,8 @@ def _pmc_traffic(path, kind, kname, B, fmt):
     return None
 
 
-def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec, folded=0):
+def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec, folded=0,
+             small=False):
     """Roofline of the dominant kernel, priced at the bytes it actually moves.
 
     Per-pass kernels (HBM-bound by design): check pass reads E message rows and writes E; variable
@@ -225,11 +228,12 @@ def roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, v
                 "note": "fused on-chip decoder: messages of 4 codewords per workgroup stay in LDS for all "
                         "iterations; LDS roofline at this kernel's 16-B read/write mix (MI355X_MICROARCH.md §LDS)",
                 "launches": {"fused": cn_n}}
+    sfx = "_small" if small else ""
     if vn_ms >= cn_ms:
-        kname = "ib_vn_fast" if fmt == "u4" else ("ib_vn_gen" if a.kind == "ib" else "fl_vn")
+        kname = ("ib_vn_small" if small else "ib_vn_fast") if fmt == "u4" else ("ib_vn_gen" if a.kind == "ib" else "fl_vn" + sfx)
         kavg, ku8 = vn_avg, vn_bytes_u8
     else:
-        kname = "ib_cn_fast" if fmt == "u4" else ("ib_cn_gen" if a.kind == "ib" else "fl_cn")
+        kname = ("ib_cn_small" if small else "ib_cn_fast") if fmt == "u4" else ("ib_cn_gen" if a.kind == "ib" else "fl_cn" + sfx)
         kavg, ku8 = cn_avg, cn_bytes_u8
     kbytes = int(ku8 * ws / w)
     t = kavg * 1e-3
@@ -591,7 +595,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
-    timing_on(True)
+    timing_on(not a.no_kernel_events)
     t0 = time.perf_counter()
     for k in range(a.steps):
         step_k[0] = k
@@ -623,7 +627,7 @@ def main():
     if a.kind == "ib":
         dtype = fmt
     roof = roofline(a, g, n_v, B, I, w, ws, fmt, match, fused, cn_avg, vn_avg, cn_ms, vn_ms, cn_n, vn_n, dec,
-                    folded=folded)
+                    folded=folded, small=small)
     # HBM bytes the decode moves per codeword at the stored widths (channel in, output out: u8 for IB, fp32 float)
     moved = moved_bytes_per_cw(g.n_e, n_v, I, "fused" if fused else "passes", ws, w, w, w_stage=w, folded=folded)
     cpu = None

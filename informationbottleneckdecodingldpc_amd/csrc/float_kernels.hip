@@ -27,13 +27,19 @@
 
 namespace ibl {
 
-// Work-item geometry from the hardware registers and the dispatch packet. This source is built with the
-// IEEE mode off (_build.py), an attribute the device libraries do not share, so HIP's threadIdx /
+// Work-item geometry from the hardware registers and the implicit kernel arguments. This source is built with
+// the IEEE mode off (_build.py), an attribute the device libraries do not share, so HIP's threadIdx /
 // blockIdx / blockDim / gridDim — calls into them — would stay out-of-line calls in every kernel.
+// The grid size is the implicit argument hidden_block_count_x (code object v5: offset 0), in the kernarg
+// segment. __builtin_amdgcn_grid_size_x() reads the AQL dispatch packet instead, which lives in the queue's
+// ring buffer in host memory: every CU's first wave then waits on a host round trip, ~20 us of every launch
+// (round 6: the float small-batch passes took 23-32 us at B = 2, the IB ones 7-9 us).
 __device__ __forceinline__ int fl_tid() { return (int)__builtin_amdgcn_workitem_id_x(); }
 __device__ __forceinline__ int fl_bid() { return (int)__builtin_amdgcn_workgroup_id_x(); }
 __device__ __forceinline__ int fl_bdim() { return (int)__builtin_amdgcn_workgroup_size_x(); }
-__device__ __forceinline__ int fl_gdim() { return (int)(__builtin_amdgcn_grid_size_x() / __builtin_amdgcn_workgroup_size_x()); }
+__device__ __forceinline__ int fl_gdim() {
+  return *(cint32*)__builtin_amdgcn_implicitarg_ptr();   // constant address space, as the pointer is
+}
 
 template <typename F> struct Vec;
 template <> struct Vec<float> {
@@ -847,7 +853,10 @@ __global__ void fl_send(FlArgs a) {
 // Vec<F>::N codewords, each lane gathering its node's 16-byte pieces of its rows. The node bodies are the
 // per-pass kernels' (fl_cn_body / fl_vn_body on the lane's N codewords, same operations in the same order),
 // so outputs equal the per-pass path's bit for bit. No fold (the small path runs every variable update).
-template <class Args, class Body>
+// A task record {first position, count, degree, contiguous} with contiguous = st0 + 1 says its nodes are
+// consecutive with edges st0 + k·d (every DVB-S2 task; plan.h order_tasks): the lane's first edge then needs
+// no load and its node (NODE: variable passes) one scalar load per task, as in the IB small-batch kernels.
+template <bool NODE, class Args, class Body>
 __device__ __forceinline__ void fl_small_items(const Args& a, int lane, Body&& body) {
   const int wpb = fl_bdim() >> 6;
   const int gw = __builtin_amdgcn_readfirstlane(fl_bid() * wpb + (fl_tid() >> 6));
@@ -856,7 +865,18 @@ __device__ __forceinline__ void fl_small_items(const Args& a, int lane, Body&& b
     const int t = __builtin_amdgcn_readfirstlane(item / a.nwords);
     const int c = __builtin_amdgcn_readfirstlane(item - t * a.nwords);
     const int p0 = sload(a.task, 4 * t), cnt = sload(a.task, 4 * t + 1), d = sload(a.task, 4 * t + 2);
-    if (lane < cnt) body(p0 + lane, c, d);
+    const int st1 = sload(a.task, 4 * t + 3);
+    if (lane < cnt) {
+      int node = 0, st;
+      if (st1 != 0) {   // wave-uniform
+        st = st1 - 1 + lane * d;
+        if constexpr (NODE) node = sload(a.info, 4 * p0) + lane;
+      } else {
+        st = a.info[4 * (p0 + lane) + 1];
+        if constexpr (NODE) node = a.info[4 * (p0 + lane)];
+      }
+      body(node, st, c, d);
+    }
   }
 }
 
@@ -870,10 +890,9 @@ __device__ __forceinline__ void fl_load_piece(const void* base, int ldb, int row
 
 template <int KIND, typename F, int D>
 __device__ __forceinline__ void fl_cn_small_item(const FlArgs& a, int st, int cw0, bool do_par, bool& unsat) {
-  constexpr int N = Vec<F>::N;
   const F lm = (F)a.llr_max;
   int tg[D];
-  F m[D][N];
+  F m[D][Vec<F>::N];
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     tg[j] = a.tgt[st + j];
@@ -882,26 +901,25 @@ __device__ __forceinline__ void fl_cn_small_item(const FlArgs& a, int st, int cw
   if (do_par) {
     const int valid = a.B - cw0;
 #pragma unroll
-    for (int s = 0; s < N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
+    for (int s = 0; s < Vec<F>::N; ++s) unsat |= syndrome_bit<F, D>(m, s) && s < valid;
   }
-  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+  fl_cn_body<KIND, F, D>(m, lm, [&](int w, const F (&o)[Vec<F>::N]) __attribute__((always_inline)) {
     fl_store_to<F>(a.out, a.ldb, tg[w], cw0, o);
   });
 }
 
 template <typename F, int D>
 __device__ __forceinline__ void fl_vn_small_item(const FlArgs& a, int node, int st, int cw0) {
-  constexpr int N = Vec<F>::N;
   const F lm = (F)a.llr_max;
   int tg[D];
-  F c[N], m[D][N];
+  F c[Vec<F>::N], m[D][Vec<F>::N];
   fl_load_piece<F>(a.ch, a.ldb, node, cw0, c);
 #pragma unroll
   for (int j = 0; j < D; ++j) {
     tg[j] = a.tgt[st + j];
     fl_load_piece<F>(a.in, a.ldb, st + j, cw0, m[j]);
   }
-  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[N]) __attribute__((always_inline)) {
+  fl_vn_body<F, D>(c, m, lm, [&](int w, const F (&o)[Vec<F>::N]) __attribute__((always_inline)) {
     fl_store_to<F>(a.out, a.ldb, tg[w], cw0, o);
   });
 }
@@ -912,8 +930,8 @@ __global__ __launch_bounds__(kFlSmallBlock) void fl_cn_small(FlArgs a) {
   if (!fl_gate(a.gate, lane)) return;
   const bool do_par = a.unsat != nullptr;
   bool unsat = false;
-  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int st = a.info[4 * pos + 1], cw0 = c * Vec<F>::N;
+  fl_small_items<false>(a, lane, [&](int, int st, int c, int d) __attribute__((always_inline)) {
+    const int cw0 = c * Vec<F>::N;
     switch (d) {
 #define X(D) case D: if constexpr (D <= MAXD) fl_cn_small_item<KIND, F, D>(a, st, cw0, do_par, unsat); break;
       FL_DEG_CASES(X)
@@ -929,8 +947,8 @@ template <typename F, int MAXD>
 __global__ __launch_bounds__(kFlSmallBlock) void fl_vn_small(FlArgs a) {
   const int lane = fl_tid() & 63;
   if (!fl_gate(a.gate, lane)) return;
-  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int node = a.info[4 * pos], st = a.info[4 * pos + 1], cw0 = c * Vec<F>::N;
+  fl_small_items<true>(a, lane, [&](int node, int st, int c, int d) __attribute__((always_inline)) {
+    const int cw0 = c * Vec<F>::N;
     switch (d) {
       case 1: fl_vn_small_item<F, 1>(a, node, st, cw0); break;
 #define X(D) case D: if constexpr (D <= MAXD) fl_vn_small_item<F, D>(a, node, st, cw0); break;
@@ -944,24 +962,22 @@ __global__ __launch_bounds__(kFlSmallBlock) void fl_vn_small(FlArgs a) {
 // APP LLR of the small path: ch + every input in ascending edge order, unclamped (as fl_dec)
 template <typename F>
 __global__ __launch_bounds__(kFlSmallBlock) void fl_dec_small(FlDecArgs a) {
-  using V = Vec<F>;
-  constexpr int N = V::N;
   const int L = __builtin_amdgcn_readfirstlane(*a.iters);
   const void* vin = (L & 1) ? a.vin1 : a.vin0;
   const int lane = fl_tid() & 63;
-  fl_small_items(a, lane, [&](int pos, int c, int d) __attribute__((always_inline)) {
-    const int node = a.info[4 * pos], st = a.info[4 * pos + 1], cw0 = c * N;
-    F x[N], r[N];
+  fl_small_items<true>(a, lane, [&](int node, int st, int c, int d) __attribute__((always_inline)) {
+    const int cw0 = c * Vec<F>::N;
+    F x[Vec<F>::N], r[Vec<F>::N];
     fl_load_piece<F>(a.ch, a.ldb, node, cw0, x);
     if (L > 0)
       for (int v = 0; v < d; ++v) {
         fl_load_piece<F>(vin, a.ldb, st + v, cw0, r);
 #pragma unroll
-        for (int s = 0; s < N; ++s) x[s] = x[s] + r[s];
+        for (int s = 0; s < Vec<F>::N; ++s) x[s] = x[s] + r[s];
       }
     const size_t o = (size_t)node * a.B + cw0;
 #pragma unroll
-    for (int s = 0; s < N; ++s) {
+    for (int s = 0; s < Vec<F>::N; ++s) {
       if (cw0 + s >= a.B) break;
       if (a.out_dtype == kF32) reinterpret_cast<float*>(a.out)[o + s] = (float)x[s];
       else reinterpret_cast<double*>(a.out)[o + s] = (double)x[s];

@@ -572,6 +572,8 @@ def test_dropin_bp_raises_on_invalid_channel(wlan_H):
     ("dvb", 12, 2, False, 1.0),        # the reference DVB-S2 driver's batch
     ("dvb", 30, 33, True, 2.0),        # ragged last word, early stop
     ("mixed", 6, 9, True, 2.0),        # every check degree 2..16, variable degree 1..16
+    ("mixed", 6, 3, True, 2.0),        # every degree, tasks not contiguous, one word
+    ("wlan", 10, 1, False, 1.5),       # B = 1
     ("wlan", 20, 70, True, 1.5)])      # forced onto the small kernels past the default threshold
 def test_float_small_batch_kernels(eng, prec, kind, name, imax, B, early, ebn0, wlan_H, dvb_H):
     """The small-batch float kernels (fl_*_small: wave item = up to 64 same-degree nodes x one 16-byte word) give
