@@ -108,7 +108,7 @@ int ibl_ib_path_in_use(const ibl_ib* h, int32_t* fused);
  * kernels).  The per-pass fast kernels give every wave one node x 1024 codewords, so a batch of a few
  * codewords — the reference's DVB-S2 driver decodes msg_at_time = 2 (BER_simulation_OpenCL.py:71) —
  * costs what B = 1024 costs; batches B <= max_b instead run kernels whose wave item is up to 64 nodes
- * of one degree (lane = node) x 8 codewords.  Default max_b = 192 (IBL_SMALL_B in the environment when
+ * of one degree (lane = node) x 8 codewords.  Default max_b = 224 (IBL_SMALL_B in the environment when
  * the decoder is created overrides it); 0 turns them off.  The fused on-chip path, when in use, ignores
  * this.  IBL_EUNSUPPORTED if max_b > 0 and the decoder has no fast path.
  */

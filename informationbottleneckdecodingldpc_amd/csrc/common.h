@@ -265,7 +265,7 @@ constexpr int kSmallBlock = 1024;
 // (B <= 8) 256 threads — more blocks stage their tables in parallel; up to 8 words 512; more 1024
 __host__ __device__ constexpr int small_block(int nwords) { return nwords <= 1 ? 256 : (nwords <= 8 ? 512 : 1024); }
 constexpr int kFlSmallBlock = 256;             // float small-batch kernels (the degree-16 BP bodies need > 128 VGPRs)
-constexpr int kSmallBatchDefault = 192;   // batches up to this many codewords take the small-batch kernels
+constexpr int kSmallBatchDefault = 224;   // batches up to this many codewords take the small-batch kernels
 constexpr int kFlSmallBatchDefault = 64;  // the float decoders' default threshold
 hipError_t launch_ib_cn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);
 hipError_t launch_ib_vn_small(const IbFastArgs& a, int maxd, int grid, size_t lds, hipStream_t s);

@@ -88,11 +88,11 @@ def test_ib_small_batch_kernels(eng, name, imax, B, match, early, ebn0, dvb_H):
 
 
 def test_ib_small_batch_default_and_generic(eng, wlan_H):
-    """Default threshold 192 (measured crossover); the generic path refuses the small-batch kernels."""
+    """Default threshold 224 (measured crossover); the generic path refuses the small-batch kernels."""
     g = graph.build_graph(wlan_H)
     G = eng.Graph(g, DEV)
     tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 3)
-    assert eng.IBDecoder(G, tb, True, 16, path="passes").small_batch == 192
+    assert eng.IBDecoder(G, tb, True, 16, path="passes").small_batch == 224
     gen = eng.IBDecoder(G, tb, True, 16, force_generic=True)
     assert gen.small_batch == 0
     from informationbottleneckdecodingldpc_amd._lib import IBLError
