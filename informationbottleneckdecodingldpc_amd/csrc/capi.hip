@@ -1347,6 +1347,7 @@ int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t
   }
   if (llr)
     for (int w = 0; w < T; ++w) a.llr[w] = llr[w];
+  a.sorted = std::is_sorted(a.kthr + 1, a.kthr + T + 1) ? 1 : 0;
   a.ctr[0] = offset;
   a.key[0] = seed;
   a.bits = d_bits;

@@ -295,6 +295,7 @@ struct ChArgs {
   void* out;                // [n][ld] u8 / i32 cluster ids or f32 / f64 LLRs
   int64_t total, ld;        // n*B, output row stride (elements)
   int32_t B, T, dtype;
+  int32_t sorted;           // kthr[1..T] non-decreasing (every CDF without NaNs): the binned inversion applies
 };
 hipError_t launch_ch_sample(const ChArgs& a, hipStream_t s);
 
