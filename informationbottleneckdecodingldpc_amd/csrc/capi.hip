@@ -1347,7 +1347,22 @@ int ibl_channel_sample(const double* cdf, int32_t T, const double* llr, uint64_t
   }
   if (llr)
     for (int w = 0; w < T; ++w) a.llr[w] = llr[w];
-  a.sorted = std::is_sorted(a.kthr + 1, a.kthr + T + 1) ? 1 : 0;
+  // binned inversion (sorted thresholds): bin b of m = u 2^53 (b = m >> kChBinSh) holds base = #{w : kthr[w] < bin
+  // start} — thresholds every m of the bin exceeds — and n = #{w : kthr[w] inside the bin}, the next n indices
+#ifndef IBL_CH_BINNED
+#define IBL_CH_BINNED 1   // 0: T compares per sample (A/B, tools/variants.py chloop)
+#endif
+  a.sorted = IBL_CH_BINNED && std::is_sorted(a.kthr + 1, a.kthr + T + 1) ? 1 : 0;
+  if (a.sorted)
+    for (int b = 0; b < kChBins; ++b) {
+      const uint64_t lo = (uint64_t)b << kChBinSh, hi = lo + (1ull << kChBinSh);
+      unsigned base = 0, nin = 0;
+      for (int w = 1; w <= T; ++w) {
+        base += a.kthr[w] < lo ? 1u : 0u;
+        nin += (a.kthr[w] >= lo && a.kthr[w] < hi) ? 1u : 0u;
+      }
+      a.bin[b] = (uint16_t)(base | (nin << 8));
+    }
   a.ctr[0] = offset;
   a.key[0] = seed;
   a.bits = d_bits;

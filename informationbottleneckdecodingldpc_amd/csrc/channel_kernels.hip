@@ -50,36 +50,17 @@ __device__ __forceinline__ int invert_cdf(uint64_t m, const ChArgs& a) {
   return t < a.T ? t : a.T - 1;
 }
 
-// Binned inversion (sorted thresholds, every CDF without NaNs): bin b = m >> kBinSh (the top 10 of m's 53 bits)
-// holds base = #{w : kthr[w] < bin start} — thresholds every m of the bin exceeds — and n = #{w : kthr[w] in the
-// bin}, contiguous after base because the thresholds are sorted; t = base + #{k <= n : m > kthr[base + k]}. With T
-// thresholds in 1024 bins n is almost always 0: one LDS read per sample replaces T 64-bit compares. The table is
-// built per workgroup from the thresholds (1024 bins x T compares over 256 threads).
-constexpr int kBinSh = 43, kBins = 1 << (53 - kBinSh);
-struct ChLds {
-  uint32_t bin[kBins];        // base | n << 16
-  uint64_t thr[kMaxT + 2];    // kthr[0..T], then a sentinel
-};
-__device__ __forceinline__ void build_bins(ChLds& L, const ChArgs& a) {
-  for (int w = threadIdx.x; w <= kMaxT + 1; w += blockDim.x) L.thr[w] = w <= a.T ? a.kthr[w] : ~0ull;
-  for (int b = threadIdx.x; b < kBins; b += blockDim.x) {
-    const uint64_t lo = (uint64_t)b << kBinSh, hi = lo + (1ull << kBinSh);
-    uint32_t base = 0, n = 0;
-    for (int w = 1; w <= a.T; ++w) {
-      const uint64_t k = a.kthr[w];
-      base += k < lo ? 1u : 0u;
-      n += (k >= lo && k < hi) ? 1u : 0u;
-    }
-    L.bin[b] = base | (n << 16);
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ int invert_binned(uint64_t m, const ChLds& L, int T) {
-  const uint32_t e = L.bin[(uint32_t)(m >> kBinSh)];
-  int t = (int)(e & 0xffffu);
-  const int n = (int)(e >> 16);
-  for (int k = 1; k <= n; ++k) t += (m > L.thr[(e & 0xffffu) + k]) ? 1 : 0;
-  return t < T ? t : T - 1;
+// Binned inversion (sorted thresholds, every CDF without NaNs): the host's table (ChArgs::bin, in the kernarg
+// segment) gives for bin m >> kChBinSh (the top 10 of m's 53 bits) base = #{w : kthr[w] < bin start} and n =
+// #{w : kthr[w] in the bin}, contiguous after base because the thresholds are sorted; t = base + #{k <= n : m >
+// kthr[base + k]}. With T thresholds in 1024 bins n is almost always 0: one cached load per sample replaces T
+// 64-bit compares. No LDS: the sampler's side-stream slices stay able to co-reside with the decode kernels.
+__device__ __forceinline__ int invert_binned(uint64_t m, const ChArgs& a) {
+  const uint32_t e = a.bin[(uint32_t)(m >> kChBinSh)];
+  const int base = (int)(e & 0xffu), n = (int)(e >> 8);
+  int t = base;
+  for (int k = 1; k <= n; ++k) t += (m > a.kthr[base + k]) ? 1 : 0;
+  return t < a.T ? t : a.T - 1;
 }
 
 template <int DT>
@@ -95,10 +76,8 @@ __device__ __forceinline__ void ch_put(const ChArgs& a, int64_t o, int t) {
 // when the batch is a multiple of 4 (u8: one dword); otherwise row / column come from one division per block.
 template <int DT>
 __global__ __launch_bounds__(256) void ch_sample(ChArgs a) {
-  __shared__ ChLds L;
   const int64_t nblk = (a.total + 3) / 4;
   const bool dense = a.ld == a.B, quad = dense && (a.total & 3) == 0 && !a.bits;
-  if (a.sorted) build_bins(L, a);   // uniform branch: every thread of the block reaches the barrier
   for (int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; blk < nblk;
        blk += (int64_t)gridDim.x * blockDim.x) {
     // 256-bit counter = offset + 1 + blk (numpy increments before generating)
@@ -114,7 +93,7 @@ __global__ __launch_bounds__(256) void ch_sample(ChArgs a) {
     philox4x64_10(c, a.key[0], a.key[1]);
     int t[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) t[s] = a.sorted ? invert_binned(c[s] >> 11, L, a.T) : invert_cdf(c[s] >> 11, a);
+    for (int s = 0; s < 4; ++s) t[s] = a.sorted ? invert_binned(c[s] >> 11, a) : invert_cdf(c[s] >> 11, a);
     const int64_t i0 = blk * 4;
     if (quad) {
       if constexpr (DT == kU8) {

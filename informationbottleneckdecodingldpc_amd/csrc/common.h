@@ -286,6 +286,7 @@ hipError_t launch_ib_dec_gen(const IbGenDecArgs& a, hipStream_t s);
 hipError_t launch_finalize(const int32_t* flags, int imax, int early, int32_t* dL, int32_t* user, hipStream_t s);
 // ------------------------------------------------------------ channel generation
 constexpr int kMaxT = 64;         // largest channel alphabet of ibl_channel_sample
+constexpr int kChBinSh = 43, kChBins = 1 << (53 - kChBinSh);   // binned CDF inversion: 1024 bins of m's 53 bits
 struct ChArgs {
   uint64_t kthr[kMaxT + 1]; // floor(cdf[w] * 2^53) of the p(t | x = 0) CDF: u = m 2^-53 > cdf[w] <=> m > kthr[w]
   double llr[kMaxT];        // output_LLRs (LLR outputs)
@@ -296,6 +297,7 @@ struct ChArgs {
   int64_t total, ld;        // n*B, output row stride (elements)
   int32_t B, T, dtype;
   int32_t sorted;           // kthr[1..T] non-decreasing (every CDF without NaNs): the binned inversion applies
+  uint16_t bin[kChBins];    // sorted: per bin of m's top bits, base | n << 8 (channel_kernels.hip invert_binned)
 };
 hipError_t launch_ch_sample(const ChArgs& a, hipStream_t s);
 

@@ -7,7 +7,7 @@ count (`return_errors_all_zero`) and the host-side stop rule. One Eb/N0 point, a
 on the side stream, one host read per round); `sync_driver` the reference call sequence batch by batch; and
 `decode_only` the same decoder decoding a resident channel back to back, measured in the same process.
 
-  python tools/bench_ber.py [--batches K] [--cases c4,c4enc,c5]"""
+  python tools/bench_ber.py [--batches K] [--cases c4,c4enc,c5] [--gen-chunk 4194304,0]"""
 import argparse
 import json
 import os
@@ -19,7 +19,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(case, batches, B):
+def run(case, batches, B, gen_chunk=None):
     import torch
     from informationbottleneckdecodingldpc_amd import codes, engine, graph, tables
     from informationbottleneckdecodingldpc_amd.ber import BERConfig, run_ber
@@ -47,6 +47,8 @@ def run(case, batches, B):
         dec = BeliefPropagationDecoderClassIrregular(H, 100, 16, B)
         cfg["llr_dtype"] = torch.float32
         what = "BP fp32 i_max=100, BeliefPropagationDecoderClassIrregular"
+    if gen_chunk is not None:
+        cfg["gen_chunk"] = gen_chunk
     run_ber(dec, BERConfig(**{**cfg, "max_blocks": B}))          # warm-up: decoder, streams, allocator
     r = run_ber(dec, BERConfig(**cfg))
     rs = run_ber(dec, BERConfig(**cfg, pipeline=False))          # the reference call sequence, batch by batch
@@ -74,7 +76,7 @@ def run(case, batches, B):
                                                       "note": "cfg.pipeline=False: quantise -> decode -> count per batch"},
             "decode_only": {"value": round(dec_only, 1),
                             "note": "the same drop-in decode on a resident channel, back to back, same batches"},
-            "vs_decode_only": round(value / dec_only, 4),
+            "vs_decode_only": round(value / dec_only, 4), "gen_chunk": BERConfig(**cfg).gen_chunk,
             "errors": r.errors[0], "errors_equal_sync_driver": True, "ber": float(r.BER_vector[0])}
 
 
@@ -83,9 +85,12 @@ def main():
     p.add_argument("--batches", type=int, default=8)
     p.add_argument("--batch", type=int, default=8192)
     p.add_argument("--cases", default="c4,c4enc,c5")
+    p.add_argument("--gen-chunk", default=None, help="comma list of BERConfig.gen_chunk values to A/B (0 = one launch a batch)")
     a = p.parse_args()
+    chunks = [None] if a.gen_chunk is None else [int(x) for x in a.gen_chunk.split(",")]
     for c in a.cases.split(","):
-        print(json.dumps(run(c, a.batches if c != "c5" else max(2, a.batches // 2), a.batch)), flush=True)
+        for gc in chunks:
+            print(json.dumps(run(c, a.batches if c != "c5" else max(2, a.batches // 2), a.batch, gc)), flush=True)
 
 
 if __name__ == "__main__":
