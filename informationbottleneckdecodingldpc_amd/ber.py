@@ -182,8 +182,8 @@ class _DeviceRunner:
     read that half is done; the caller's stream waits for batch k's channel and decodes it through the drop-in
     method (``decode_OpenCL*``, return_buffer); the side stream then counts batch k's errors into slot k of a device
     vector (the rows and threshold ``return_errors_all_zero`` uses, or the transmitted bits). The host reads a
-    round's vector once (``read``) — by then ``_rank_sweep`` has enqueued the next round. IB channels are u8 cluster
-    ids (the reference's int32 holds the same values; the decoder stages a quarter of the bytes)."""
+    round's vector once (``read``) — by then ``_rank_sweep`` has enqueued the next round. IB channels and decisions
+    are u8 cluster ids (the reference's int32 holds the same values; a quarter of the bytes to write and count)."""
     lookahead = True
 
     def __init__(self, decoder, kind, quanti, tx, B, N_var, pb_ch, pb_bits, err_rows, thr, cfg):
@@ -192,6 +192,15 @@ class _DeviceRunner:
         self.decoder, self.kind, self.quanti, self.tx = decoder, kind, quanti, tx
         self.B, self.pb_ch, self.pb_bits, self.err_rows, self.thr = B, pb_ch, pb_bits, err_rows, thr
         self.gen_chunk = int(cfg.gen_chunk)
+        # u8 decisions from decoders whose decode_OpenCL takes out_dtype (this package's); others as they come
+        self.dec_kw = {}
+        if kind == "ib":
+            import inspect
+            try:
+                if "out_dtype" in inspect.signature(decoder.decode_OpenCL).parameters:
+                    self.dec_kw = {"out_dtype": torch.uint8}
+            except (TypeError, ValueError):  # pragma: no cover - builtins without a signature
+                pass
         dev = decoder.device
         self.dev = dev
         self.main = torch.cuda.current_stream(dev)
@@ -250,7 +259,7 @@ class _DeviceRunner:
             self.main.wait_event(self.ready[slot])
             with torch.cuda.stream(self.main):
                 if self.kind == "ib":
-                    dec = d.decode_OpenCL(self.ch[slot], buffer_in=True, return_buffer=True)
+                    dec = d.decode_OpenCL(self.ch[slot], buffer_in=True, return_buffer=True, **self.dec_kw)
                 else:
                     fn = d.decode_OpenCL_min_sum if self.kind == "minsum" else d.decode_OpenCL_belief_propagation
                     dec = fn(self.ch[slot], buffer_in=True, return_buffer=True)

@@ -57,14 +57,16 @@ class Discrete_LDPC_Decoder_class(CodeMixin):
         self.msg_at_time = int(msg_at_time_)
         self._dec = IBDecoder(self._graph_on(dev), self._tables(), False, self.msg_at_time)
 
-    def decode_OpenCL(self, received_blocks, buffer_in=False, return_buffer=False):
+    def decode_OpenCL(self, received_blocks, buffer_in=False, return_buffer=False, out_dtype=torch.int32):
         """Reference :202-295."""
         if self._dec is None:
             self.init_OpenCL_decoding(self.msg_at_time)
         ch = to_device_input(received_blocks, buffer_in, self.device, (torch.int32, torch.uint8))
         if ch.shape[1] > self._dec.max_batch:
             self.init_OpenCL_decoding(ch.shape[1], self.device)
-        out = self._dec.decode(ch, out_dtype=torch.int32, early_stop=True)
+        # out_dtype: the reference's int32 cluster ids; torch.uint8 holds the same values in a quarter of the bytes
+        # (the pipelined BER driver's decisions)
+        out = self._dec.decode(ch, out_dtype=out_dtype, early_stop=True)
         return out if return_buffer else out.cpu().numpy()
 
     def return_errors_all_zero(self, varnode_output_buffer):

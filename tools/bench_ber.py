@@ -59,12 +59,14 @@ def run(case, batches, B, gen_chunk=None):
     x = torch.empty((g.n_v, B), dtype=torch.uint8 if case.startswith("c4") else torch.float32, device="cuda")
     q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
     engine.channel_sample(x, q.cdf_t_given_x_equals_zero, 2, 0, llr=None if case.startswith("c4") else q.output_LLRs)
+    # (IB: u8 decisions, as the pipelined driver asks for them — the same cluster ids as the reference's int32)
+    kw = {"out_dtype": torch.uint8} if case.startswith("c4") else {}
     fn = dec.decode_OpenCL if case.startswith("c4") else dec.decode_OpenCL_belief_propagation
-    fn(x, buffer_in=True, return_buffer=True)
+    fn(x, buffer_in=True, return_buffer=True, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(r.blocks[0] // B):
-        fn(x, buffer_in=True, return_buffer=True)
+        fn(x, buffer_in=True, return_buffer=True, **kw)
     torch.cuda.synchronize()
     dec_only = r.blocks[0] / (time.perf_counter() - t0)
     value = r.blocks[0] / sec
