@@ -1518,7 +1518,31 @@ __global__ __launch_bounds__(256) void ib_stage4(const void* ch, int n, int B, u
   const int64_t items = (int64_t)n * nseg;
   for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
     const int row = (int)(it / nseg);
-    const int w0 = (int)(it - (int64_t)row * nseg) * (256 * U) + (int)threadIdx.x;
+    const int seg0 = (int)(it - (int64_t)row * nseg) * (256 * U);
+    if constexpr (DT == kU8) {
+      // u8 rows of 16-byte multiples (vec == 2) and a whole item inside the row: a lane takes 4 consecutive words
+      // (32 codewords) as two 16-byte loads and one 16-byte store (1 KiB per wave instruction)
+      if (vec == 2 && seg0 + 256 * U <= words) {
+        const int w = seg0 + 4 * (int)threadIdx.x;
+        const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ch) + (size_t)row * B + 8 * (size_t)w);
+        const uint4 q0 = p[0], q1 = p[1];
+        const uint32_t d[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t e[8];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            e[s] = (d[2 * k] >> (8 * s)) & 0xffu;
+            e[4 + s] = (d[2 * k + 1] >> (8 * s)) & 0xffu;
+          }
+          o[k] = nib8(e);
+        }
+        *reinterpret_cast<uint4*>(ch4 + (size_t)row * ldb_bytes + 4 * (size_t)w) = make_uint4(o[0], o[1], o[2], o[3]);
+        continue;
+      }
+    }
+    const int w0 = seg0 + (int)threadIdx.x;
     uint32_t v[U][8];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1720,7 +1744,9 @@ hipError_t launch_ib_stage4(const void* ch, int dtype, int n, int B, uint8_t* ch
   const int64_t nseg = (words + 1023) / 1024, items = (int64_t)n * nseg;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(items, 8192));
   const size_t align = dtype == kU8 ? 8 : 16;
-  const int vec = (B % 8) == 0 && (reinterpret_cast<uintptr_t>(ch) % align) == 0;
+  int vec = (B % 8) == 0 && (reinterpret_cast<uintptr_t>(ch) % align) == 0;
+  if (vec && dtype == kU8 && (B % 16) == 0 && (reinterpret_cast<uintptr_t>(ch) % 16) == 0 && (ldb_bytes % 16) == 0)
+    vec = 2;   // 16-byte rows (ib_stage4's u8 quad-word path)
   if (dtype == kU8)
     hipLaunchKernelGGL(ib_stage4<kU8>, dim3(grid), dim3(256), 0, s, ch, n, B, ch4, ldb_bytes, words, nseg, vec);
   else

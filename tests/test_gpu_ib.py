@@ -451,6 +451,25 @@ def test_fused_lds_cap_survives_a_smaller_decoder(wlan_H):
     np.testing.assert_array_equal(o1, oracle.ib_decode(g1, tb1, x1, match=False))
 
 
+def test_u8_staging_quad_words(eng, wlan_H):
+    """The u8 channel staging's 16-byte path (rows of 16-byte multiples: whole 1024-word items; the rest of a row
+    and other rows by words) decodes what the int32 staging decodes: B = 8208 = one whole item + 2 words per row,
+    a 16-byte aligned base and one at +16 (the view's rows still 16-byte multiples), per-pass kernels."""
+    g = graph.build_graph(wlan_H)
+    tb = tables.random_tables(16, 16, g.d_c_max, g.d_v_max, 3, seed=9)
+    B = 8208
+    x = torch.from_numpy(np.random.default_rng(7).integers(0, 16, (g.n_v, B)).astype(np.uint8)).to(DEV)
+    dec = eng.IBDecoder(eng.Graph(g, DEV), tb, True, B, path="passes")
+    ref = dec.decode(x.to(torch.int32), out_dtype=torch.uint8, early_stop=False).clone()
+    np.testing.assert_array_equal(ref[:, :3].cpu().numpy(), oracle.ib_decode(g, tb, x[:, :3].cpu().numpy(), match=True))
+    out = dec.decode(x, out_dtype=torch.uint8, early_stop=False)
+    assert torch.equal(out, ref)
+    buf = torch.zeros(g.n_v * B + 16, dtype=torch.uint8, device=DEV)
+    xv = buf[16:].view(g.n_v, B)
+    xv.copy_(x)
+    assert torch.equal(dec.decode(xv, out_dtype=torch.uint8, early_stop=False), ref)
+
+
 @pytest.mark.parametrize("path", ["fused", "passes"])
 def test_misaligned_u8_channel(eng, wlan_H, path):
     """A contiguous u8 channel view at an odd byte offset (B % 4 == 0, so the staging kernels' dword path
