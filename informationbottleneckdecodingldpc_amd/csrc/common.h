@@ -79,12 +79,6 @@ __device__ __forceinline__ int32_t sload(const int32_t* p, int i) { return ((cin
 // One workgroup-wide work ticket from an LDS counter (lane 0 takes it, the wave reads it back as a
 // scalar). Persistent kernels hand each block's static item share to its waves this way: waves on a
 // SIMD issue oldest-first, so equal static per-wave shares leave a CU waiting for its youngest waves.
-// Fused kernels (ib_fused, fl_fused): each wave takes the NEXT phase's first ticket before the barrier that ends
-// the current phase (three counters in rotation: the one two phases ahead is reset while a phase runs), so the
-// contended LDS atomic is off the phase's critical path. 0 = take it after the barrier (A/B, variant pretick0).
-#ifndef IBL_FUSED_PRETICKET
-#define IBL_FUSED_PRETICKET 1
-#endif
 __device__ __forceinline__ int take_ticket(int* ctr, int lane) {
   int t = 0;
   if (lane == 0) t = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -1086,14 +1086,12 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
     L = __builtin_amdgcn_readfirstlane(*a.dL);
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
-  if (fl_tid() < 3) ctr[fl_tid()] = 0;
+  if (fl_tid() < 2) ctr[fl_tid()] = 0;
   // variable-edge slot indices, [ctr x 4][n_vs x u16] after the channel slots
   uint16_t* vs = reinterpret_cast<uint16_t*>(ctr + 4);
   for (int i = fl_tid(); i < a.n_vs; i += fl_bdim()) vs[i] = (uint16_t)a.vn_slot[i];
   __syncthreads();
   int ph = 0;
-  constexpr bool PT = IBL_FUSED_PRETICKET != 0;
-  int pend = PT ? take_ticket(ctr, lane) : 0;   // this wave's first ticket of the coming phase (PT)
   const int shard = (int)((fl_bid() * (fl_bdim() >> 6) + (fl_tid() >> 6)) & (kShards - 1));
   // one phase: tasks dealt by ticket; the next phase's counter is reset while this one runs
 #ifndef IBL_FUSED_TRACE
@@ -1196,11 +1194,11 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
 
   // ---- phases separated by barriers
   auto phase = [&](int ntasks, auto&& body) __attribute__((always_inline)) {
-    // work counter of this phase; the one two phases ahead is reset meanwhile (PT: three in rotation)
-    int* c = ctr + (PT ? ph % 3 : (ph & 1));
-    if (fl_tid() == 0) ctr[PT ? (ph + 2) % 3 : ((ph + 1) & 1)] = 0;
+    int* c = ctr + (ph & 1);
+    if (fl_tid() == 0) ctr[(ph + 1) & 1] = 0;
     int taken = 0;
-    for (int t = PT ? pend : take_ticket(c, lane);; t = take_ticket(c, lane)) {
+    for (;;) {
+      const int t = take_ticket(c, lane);
       if (t >= ntasks) break;
       if constexpr (IBL_FUSED_TRACE) {
         if (tr && taken == 0) tr[TW * ph + 33 + wv] = __builtin_readcyclecounter();
@@ -1217,7 +1215,6 @@ __global__ __launch_bounds__((fl_fused_block_of<CMAX, KIND, F>())) void fl_fused
         tr[TW * ph + 17 + wv] = (uint64_t)taken;
       }
     }
-    if constexpr (PT) pend = take_ticket(ctr + (ph + 1) % 3, lane);   // the next phase's first ticket
     __syncthreads();
     ++ph;
     if constexpr (IBL_FUSED_TRACE) {

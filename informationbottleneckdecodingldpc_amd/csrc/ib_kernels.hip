@@ -1260,19 +1260,9 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     L = __builtin_amdgcn_readfirstlane(*a.dL);
     if (L >= a.imax - 1) return;   // no early stop happened: pass 1's outputs stand
   }
-  if (threadIdx.x < 3) ctr[threadIdx.x] = 0;
+  if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
   __syncthreads();
   int ph = 0;
-  constexpr bool PT = IBL_FUSED_PRETICKET != 0;
-  int pend = PT ? take_ticket(ctr, lane) : 0;   // this wave's first ticket of the coming phase (PT)
-  // the phase's work counter, and the one reset while it runs (two phases ahead; PT: three in rotation)
-  auto cur_ctr = [&]() __attribute__((always_inline)) { return ctr + (PT ? ph % 3 : (ph & 1)); };
-  auto reset_ahead = [&]() __attribute__((always_inline)) {
-    if (threadIdx.x == 0) ctr[PT ? (ph + 2) % 3 : ((ph + 1) & 1)] = 0;
-  };
-  auto pretake = [&]() __attribute__((always_inline)) {   // before the barrier that ends phase ph
-    if constexpr (PT) pend = take_ticket(ctr + (ph + 1) % 3, lane);
-  };
   const int shard = (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kShards - 1));
   TablePrefetch pf;
   pf.dbuf = a.dbuf != 0;
@@ -1286,7 +1276,6 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
     }
   };
   auto next_phase = [&]() __attribute__((always_inline)) {
-    pretake();
     if (pf.dbuf) {
       pf.put_set(lds, ((ph + 1) & 1) ? a.nreg : 0);
       __syncthreads();
@@ -1306,9 +1295,10 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   };
   // check tasks: slots are contiguous per task (no index loads)
   auto cn_phase = [&](bool do_par, uint32_t vmask, bool& unsat) __attribute__((always_inline)) {
-    int* c = cur_ctr();
-    reset_ahead();
-    for (int t = PT ? pend : take_ticket(c, lane);; t = take_ticket(c, lane)) {
+    int* c = ctr + (ph & 1);
+    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
+    for (;;) {
+      const int t = take_ticket(c, lane);
       if (t >= a.n_cn_tasks) break;
       int first, cnt, d;
       if (a.cn_uni) {
@@ -1333,11 +1323,11 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
   // variable tasks (send / VN pass / decision): task k+1's indices and channel are fetched before task
   // k is computed (ping-pong buffers, unconditional clamped prefetch: straight-line waits)
   auto vn_phase = [&](const uint32_t* chg, uint32_t csh, auto&& body) __attribute__((always_inline)) {
-    int* c = cur_ctr();
-    reset_ahead();
+    int* c = ctr + (ph & 1);
+    if (threadIdx.x == 0) ctr[(ph + 1) & 1] = 0;
     const int last = a.n_vn_tasks - 1;
     VnTask<MAXD> A, Bb;
-    int t = PT ? pend : take_ticket(c, lane);
+    int t = take_ticket(c, lane);
     if (t > last) return;
     fetch_vn_task(a, chg, t, lane, A, csh);
     for (;;) {
@@ -1408,7 +1398,6 @@ __global__ __launch_bounds__(CMAX <= 8 && VMAX <= 8 ? 1024 : 512) void ib_fused(
       store4(a.out, a.out_dtype, o, 0, a.B - cwb, a.aligned != 0, r[0]);
       if constexpr (NCW == 8) store4(a.out, a.out_dtype, o, 4, a.B - cwb, a.aligned != 0, r[1]);
     });
-    pretake();
     __syncthreads();   // every wave done with this group's slots before the next group's send
     mark(3 * ph + 1);
     ++ph;

@@ -26,9 +26,7 @@ VARIANTS = {
     "mix1": ["IBL_MIX16=4"],
     # round 6: every wave interleaves one heavy and two light variable items (ib_phase_mix3)
     "vmix3": ["IBL_VN_MIX3=1"],
-    "chloop": ["IBL_CH_BINNED=0"],
-    "pretick0": ["IBL_FUSED_PRETICKET=0"],   # fused kernels take each phase's first ticket after its barrier
-    "ftrace0": ["IBL_FUSED_TRACE=1", "IBL_DIAG=1", "IBL_FUSED_PRETICKET=0"],   # channel sampler: T compares per sample (before round 6's binned inversion)
+    "chloop": ["IBL_CH_BINNED=0"],   # channel sampler: T compares per sample (before round 6's binned inversion)
     "mix2": ["IBL_MIX16=8"],
     "mix3": ["IBL_MIX16=12"],
     "mixw2": ["IBL_MIX16=2"],
