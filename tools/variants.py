@@ -26,7 +26,9 @@ VARIANTS = {
     "mix1": ["IBL_MIX16=4"],
     # round 6: every wave interleaves one heavy and two light variable items (ib_phase_mix3)
     "vmix3": ["IBL_VN_MIX3=1"],
-    "chloop": ["IBL_CH_BINNED=0"],   # channel sampler: T compares per sample (before round 6's binned inversion)
+    "chloop": ["IBL_CH_BINNED=0"],
+    "ntcn0": ["IBL_NT_CN=0"],   # check pass rows with the default cache policy (round 5 adopted nontemporal)
+    "mix0": ["IBL_MIX16=0"],    # no light-first waves in the variable pass (round 5 adopted 4 of 16)   # channel sampler: T compares per sample (before round 6's binned inversion)
     "mix2": ["IBL_MIX16=8"],
     "mix3": ["IBL_MIX16=12"],
     "mixw2": ["IBL_MIX16=2"],
