@@ -713,9 +713,11 @@ __device__ __forceinline__ void ib_pass(const IbFastArgs& a, const uint8_t* lds)
   // block's waves take the light share first, so both kinds run side by side on every CU; a wave that
   // exhausts its first share joins the other (two ticket counters). Round 5, quad layout (heavy items
   // now 0.239 ms alone, light 0.2405 ms, together 0.436 ms; profiles/r05_vn_mix_ab.json): a quarter of
-  // the waves light-first measured VN 0.4205 ms against 0.433 ms for half (the round-2 choice).
+  // the waves light-first measured VN 0.4205 ms against 0.433 ms for half (the round-2 choice). Round 6, three
+  // alternating repetitions on each of two boxes (profiles/r06_light_first_share_sweep_*.txt): 6 of 16 beat 4 of
+  // 16 in all six (C4 +0.26 % / +0.4 %, VN -1 % / -1.5 %); 3, 5, 8 and 10 did not.
 #ifndef IBL_MIX16
-#define IBL_MIX16 4
+#define IBL_MIX16 6
 #endif
   const bool light_first = VN && (int)(threadIdx.x >> 6) * 16 < wpb * IBL_MIX16;
   if constexpr (VN && MAXD <= 8 && IBL_VN_MIX3) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session ab: light-first share of the C4 variable pass (IBL_MIX16 of 16 waves), 3 alternating reps.
 set -o pipefail
-O=gpurun_out/r6ab
+O=gpurun_out/${TAG:-r6ab}
 mkdir -p $O
 V=informationbottleneckdecodingldpc_amd/variants
 run() {
@@ -11,7 +11,7 @@ run() {
 }
 for rep in 1 2 3; do
   run base4_$rep "" --config C4
-  run mix3_$rep $V/libibldpc_mixw3.so --config C4
-  run mix5_$rep $V/libibldpc_mixw5.so --config C4
-  run mix6_$rep $V/libibldpc_mixw6.so --config C4
+  for m in ${MIXES:-mixw3 mixw5 mixw6}; do
+    run ${m}_$rep $V/libibldpc_$m.so --config C4
+  done
 done

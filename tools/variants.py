@@ -29,7 +29,8 @@ VARIANTS = {
     "chloop": ["IBL_CH_BINNED=0"],
     "ntcn0": ["IBL_NT_CN=0"],   # check pass rows with the default cache policy (round 5 adopted nontemporal)
     "mix0": ["IBL_MIX16=0"],
-    "mixw5": ["IBL_MIX16=5"],    # no light-first waves in the variable pass (round 5 adopted 4 of 16)   # channel sampler: T compares per sample (before round 6's binned inversion)
+    "mixw5": ["IBL_MIX16=5"],
+    "mixw10": ["IBL_MIX16=10"],    # no light-first waves in the variable pass (round 5 adopted 4 of 16)   # channel sampler: T compares per sample (before round 6's binned inversion)
     "mix2": ["IBL_MIX16=8"],
     "mix3": ["IBL_MIX16=12"],
     "mixw2": ["IBL_MIX16=2"],
