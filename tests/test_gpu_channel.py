@@ -47,6 +47,26 @@ def test_channel_sample_bits_and_alphabets(T):
     assert np.array_equal(out.cpu().numpy(), oracle.channel_sample(q.cdf_t_given_x_equals_zero, 5, 11, n, B, bits))
 
 
+@pytest.mark.parametrize("case", ["clustered", "ties", "unsorted", "nan"])
+def test_channel_sample_cdf_shapes(case):
+    """The binned inversion (sorted thresholds: one table load per sample, compares only in bins holding
+    thresholds) and its fallback (unsorted or NaN CDFs: T compares) equal the oracle's direct count: thresholds
+    packed into one bin (many compares in it), repeated values, a decreasing entry, a NaN entry."""
+    T = 16
+    if case == "clustered":
+        cdf = np.concatenate([[0.0], 0.5 + 1e-7 * np.arange(T - 1), [1.0]])
+    elif case == "ties":
+        cdf = np.concatenate([[0.0], np.repeat([0.25, 0.5, 0.75], 5), [1.0]])
+    else:
+        cdf = np.linspace(0.0, 1.0, T + 1)
+        cdf[7] = 0.2 if case == "unsorted" else np.nan
+    n, B = 64, 515
+    out = torch.empty((n, B), dtype=torch.int32, device=DEV)
+    engine.channel_sample(out, cdf, 12, 3)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.channel_sample(cdf, 12, 3, n, B))
+
+
 def test_channel_batches_continue_the_stream():
     q = _q()
     cdf = q.cdf_t_given_x_equals_zero
