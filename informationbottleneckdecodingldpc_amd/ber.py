@@ -65,6 +65,7 @@ class BERConfig:
     encoded: bool = False                 # random encoded codewords (LDPC_BPSK_Transmitter) instead of all-zero
     pipeline: bool = True                 # device double buffering + side-stream counts (see the module docstring)
     gen_chunk: int = 1 << 22              # pipelined channel: samples per side-stream launch (0 = one launch a batch)
+    side_stream_min: int = 1 << 20        # pipelined batches of fewer channel samples stay on one stream (no events)
 
 
 @dataclass
@@ -183,7 +184,10 @@ class _DeviceRunner:
     method (``decode_OpenCL*``, return_buffer); the side stream then counts batch k's errors into slot k of a device
     vector (the rows and threshold ``return_errors_all_zero`` uses, or the transmitted bits). The host reads a
     round's vector once (``read``) — by then ``_rank_sweep`` has enqueued the next round. IB channels and decisions
-    are u8 cluster ids (the reference's int32 holds the same values; a quarter of the bytes to write and count)."""
+    are u8 cluster ids (the reference's int32 holds the same values; a quarter of the bytes to write and count).
+    Batches of fewer than ``cfg.side_stream_min`` channel samples (the reference DVB-S2 driver's msg_at_time = 2)
+    have little to overlap and many short launches: they run on the caller's stream alone, in the same order and
+    with the same per-round host read, without the cross-stream events."""
     lookahead = True
 
     def __init__(self, decoder, kind, quanti, tx, B, N_var, pb_ch, pb_bits, err_rows, thr, cfg):
@@ -204,14 +208,16 @@ class _DeviceRunner:
         dev = decoder.device
         self.dev = dev
         self.main = torch.cuda.current_stream(dev)
-        self.side = torch.cuda.Stream(dev)
+        self.single = N_var * B < int(cfg.side_stream_min)
+        self.side = self.main if self.single else torch.cuda.Stream(dev)
         ch_dtype = torch.uint8 if kind == "ib" else (cfg.llr_dtype or torch.float64)
         with torch.cuda.stream(self.side):
             self.ch = [torch.empty((N_var, B), dtype=ch_dtype, device=dev) for _ in range(2)]
             if tx is not None:
                 self.info = [torch.empty((tx.K, B), dtype=torch.uint8, device=dev) for _ in range(2)]
                 self.code = [torch.empty((N_var, B), dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.side.wait_stream(self.main)        # the buffers exist before the side stream writes them
+        if not self.single:
+            self.side.wait_stream(self.main)    # the buffers exist before the side stream writes them
         self.used = [None, None]                # event: the decode that last read each half is done
         self.ready = [None, None]
         self.slot_g = [None, None]              # global batch whose channel a half holds (None: consumed)
@@ -221,7 +227,7 @@ class _DeviceRunner:
         from .engine import channel_sample, random_bits
         torch, q = self.torch, self.quanti
         with torch.cuda.stream(self.side):
-            if self.used[slot] is not None:
+            if self.used[slot] is not None:     # (one stream: the decode precedes in stream order)
                 self.side.wait_event(self.used[slot])
             bits = None
             if self.tx is not None:
@@ -240,8 +246,10 @@ class _DeviceRunner:
                 r1 = min(n, r0 + rows)
                 channel_sample(out[r0:r1], q.cdf_t_given_x_equals_zero, q.seed, g * self.pb_ch + (r0 * B) // 4,
                                llr=llr, bits=None if bits is None else bits[r0:r1])
-            ev = torch.cuda.Event()
-            ev.record(self.side)
+            ev = None
+            if not self.single:
+                ev = torch.cuda.Event()
+                ev.record(self.side)
         self.ready[slot], self.slot_g[slot] = ev, g
 
     def enqueue(self, gs, next_g=None):
@@ -256,19 +264,23 @@ class _DeviceRunner:
             ng = gs[i + 1] if i + 1 < len(gs) else next_g
             if ng is not None and self.slot_g[1 - slot] != ng:
                 self._gen(1 - slot, ng)         # batch k+1's channel while batch k decodes
-            self.main.wait_event(self.ready[slot])
+            if self.ready[slot] is not None:
+                self.main.wait_event(self.ready[slot])
             with torch.cuda.stream(self.main):
                 if self.kind == "ib":
                     dec = d.decode_OpenCL(self.ch[slot], buffer_in=True, return_buffer=True, **self.dec_kw)
                 else:
                     fn = d.decode_OpenCL_min_sum if self.kind == "minsum" else d.decode_OpenCL_belief_propagation
                     dec = fn(self.ch[slot], buffer_in=True, return_buffer=True)
-                ev = torch.cuda.Event()
-                ev.record(self.main)
+                ev = None
+                if not self.single:
+                    ev = torch.cuda.Event()
+                    ev.record(self.main)
             self.used[slot], self.slot_g[slot] = ev, None
             with torch.cuda.stream(self.side):
-                self.side.wait_event(ev)
-                dec.record_stream(self.side)
+                if ev is not None:
+                    self.side.wait_event(ev)
+                    dec.record_stream(self.side)
                 if self.tx is None:
                     count_below(dec, self.err_rows, self.thr, out=cnt[i:i + 1])
                 else:

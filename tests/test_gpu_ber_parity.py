@@ -178,14 +178,16 @@ def test_bp_c5_sweep_world_size_invariant(dvb_H):
     assert ref[3][0] < cfg.max_blocks and ref[3][-1] == cfg.max_blocks   # both stop rules exercised
 
 
+@pytest.mark.parametrize("side", [0, None])   # 0: side stream at every batch size; None: the default threshold
 @pytest.mark.parametrize("case", ["ib", "ib_encoded", "bp32", "lockstep2"])
-def test_pipelined_driver_equals_sync_driver(case, wlan_H, dvb_H):
+def test_pipelined_driver_equals_sync_driver(case, side, wlan_H, dvb_H):
     """the pipelined BER driver (``_DeviceRunner``: channel of batch k+1 generated on a side stream
     into a double buffer while batch k decodes, error counts on the side stream, counts read once per round with the
     next round already enqueued) counts exactly the frames and errors of the reference call sequence
     (``cfg.pipeline=False``: quantise -> decode -> return_errors_all_zero per batch) — min_errors stops inside a
     round (the lookahead round is discarded), max_blocks ends the last points; encoded codewords; BP fp32; two
-    emulated ranks sharing one decoder."""
+    emulated ranks sharing one decoder. Both pipelined modes: side stream + events, and (batches below
+    ``side_stream_min``, as these are by default) the caller's stream alone."""
     from informationbottleneckdecodingldpc_amd.ber import run_ber_lockstep
     from informationbottleneckdecodingldpc_amd.bp_decoder_irreg import BeliefPropagationDecoderClassIrregular
     from informationbottleneckdecodingldpc_amd.discrete_LDPC_decoder_irreg import \
@@ -206,6 +208,8 @@ def test_pipelined_driver_equals_sync_driver(case, wlan_H, dvb_H):
         dec = Discrete_LDPC_Decoder_class_irregular(H, 15, 16, 16, tb.cn, tb.vn, tb.match_cn, tb.match_vn, B,
                                                     match="true")
     res = {}
+    if side is not None:
+        kw["side_stream_min"] = side
     for pipe in (True, False):
         cfg = BERConfig(**kw, pipeline=pipe)
         res[pipe] = run_ber_lockstep(dec, cfg, 2) if case == "lockstep2" else run_ber(dec, cfg)
