@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <functional>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -142,6 +143,53 @@ struct KCfg {
   size_t lds = 0;
 };
 
+// Small-batch pass chains replayed from captured graphs. A decode of a few codewords is ~2 i_max dependent launches
+// of a few microseconds each; launching them one by one costs the host about as much as the GPU spends running
+// them, so a caller that does anything else per batch (the BER driver) leaves the GPU waiting. The chain between
+// channel staging and the stop-iteration / decision kernels touches only the decoder's own buffers, so it is
+// captured once per (batch, early stop) on a private stream and replayed on the caller's stream with one call.
+struct ChainGraphs {
+  hipStream_t cap = nullptr;
+  std::map<std::pair<int, int>, hipGraphExec_t> execs;
+  bool on = false;
+  void clear() {
+    for (auto& e : execs) (void)hipGraphExecDestroy(e.second);
+    execs.clear();
+  }
+  ~ChainGraphs() {
+    clear();
+    if (cap) (void)hipStreamDestroy(cap);
+  }
+  // run chain(stream) for key on stream s: replay its graph, capturing it first if needed
+  template <class F>
+  hipError_t run(int B, int early, hipStream_t s, F&& chain) {
+    const auto key = std::make_pair(B, early);
+    auto it = execs.find(key);
+    if (it == execs.end()) {
+      if (!cap) {
+        const hipError_t e = hipStreamCreateWithFlags(&cap, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+      }
+      if (execs.size() >= 64) clear();   // bounded: at most 64 batch sizes kept
+      hipError_t e = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+      if (e != hipSuccess) return e;
+      const hipError_t ec = chain(cap);
+      hipGraph_t graph = nullptr;
+      e = hipStreamEndCapture(cap, &graph);
+      if (ec != hipSuccess || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return ec != hipSuccess ? ec : e;
+      }
+      hipGraphExec_t exec = nullptr;
+      e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(graph);
+      if (e != hipSuccess) return e;
+      it = execs.emplace(key, exec).first;
+    }
+    return hipGraphLaunch(it->second, s);
+  }
+};
+
 struct ibl_ib {
   const ibl_graph* g = nullptr;
   int32_t Tc = 0, T = 0, imax = 0, CM = 0, VM = 0, match = 0, max_batch = 0, ldb = 0;
@@ -165,6 +213,7 @@ struct ibl_ib {
   int32_t small_b = 0;
   bool s_ok = false;                          // the small-batch kernels exist for this decoder and run without scratch
   size_t s_lds_cn = 0, s_lds_vn = 0, s_lds_dec = 0;
+  ChainGraphs s_graphs;                       // small-batch pass chains (IBL_SMALL_GRAPH=0 at create: launch them)
   int32_t *f_cn_task = nullptr, *f_vn_task = nullptr, *f_vn_node = nullptr, *f_vn_slot = nullptr;
   int32_t f_ncn = 0, f_nvn = 0, f_nreg = 0, f_dbuf = 0, f_cn_uni = 0, f_vn_uni = 0;
   size_t f_lds = 0;
@@ -190,6 +239,7 @@ struct ibl_float {
   int32_t* bad = nullptr;   // channel LLRs that violated the precondition since the last ibl_float_input_check
   int32_t small_b = 0;      // small-batch kernels (fl_*_small) for B <= small_b (0: off)
   bool s_ok = false;        // the small-batch kernels run without scratch (create's check)
+  ChainGraphs s_graphs;     // small-batch pass chains (IBL_SMALL_GRAPH=0 at create: launch them one by one)
   KTimer timer;
   // fused on-chip path (FlFusedArgs): task tables, LDS bytes per workgroup, grid
   int32_t path = IBL_PATH_AUTO;
@@ -559,6 +609,8 @@ int ibl_ib_create(const ibl_graph* g, int32_t Tc, int32_t T, int32_t imax, const
       const char* sb = getenv("IBL_SMALL_B");
       h->s_ok = priv == 0;
       h->small_b = h->s_ok ? (sb ? std::max(0, atoi(sb)) : kSmallBatchDefault) : 0;
+      const char* sg = getenv("IBL_SMALL_GRAPH");
+      h->s_graphs.on = !(sg && sg[0] == '0');
       h->s_lds_cn = lds_of_quads(h->cn_nt);
       h->s_lds_vn = lds_of_quads(h->vn_nt);
       h->s_lds_dec = lds_of_quads(h->dec_nt);
@@ -740,20 +792,32 @@ int ibl_ib_decode(ibl_ib* h, const void* d_ch, int32_t ch_dtype, int32_t B, void
     std::memcpy(cn.fslot, h->cn_fslot, sizeof(cn.fslot));
     std::memcpy(vn.fslot, h->vn_fslot, sizeof(vn.fslot));
     const int gcn = grid_of(g->n_cn_task, h->s_lds_cn), gvn = grid_of(g->n_vn_task, h->s_lds_vn);
-    cn.in = nullptr; cn.gather = g->csr_cols; cn.img = h->cn_img; cn.gate = nullptr; cn.unsat = nullptr;
-    HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
-    cn.gather = nullptr;
-    cn.in = h->cin;
-    for (int j = 1; j < I; ++j) {
-      const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-      vn.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
-      vn.gate = gate;
-      HIPCHK(h->timer.timed(1, s, [&] { return launch_ib_vn_small(vn, h->VM, gvn, h->s_lds_vn, s); }));
-      cn.img = h->cn_img + (size_t)j * h->cn_nt * 256;
-      cn.gate = gate;
-      cn.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
-      HIPCHK(h->timer.timed(0, s, [&] { return launch_ib_cn_small(cn, h->CM, gcn, h->s_lds_cn, s); }));
-    }
+    // the pass chain (decoder buffers only): CN pass 0 from the staged channel, then {VN j, CN j}
+    auto chain = [&](hipStream_t st) -> hipError_t {
+      IbFastArgs c0 = cn, v = vn;
+      c0.in = nullptr; c0.gather = g->csr_cols; c0.img = h->cn_img; c0.gate = nullptr; c0.unsat = nullptr;
+      hipError_t e = h->timer.timed(0, st, [&] { return launch_ib_cn_small(c0, h->CM, gcn, h->s_lds_cn, st); });
+      if (e != hipSuccess) return e;
+      IbFastArgs c = c0;
+      c.gather = nullptr;
+      c.in = h->cin;
+      for (int j = 1; j < I; ++j) {
+        const int32_t* gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+        v.img = h->vn_img + (size_t)(j - 1) * h->vn_nt * 256;
+        v.gate = gate;
+        if ((e = h->timer.timed(1, st, [&] { return launch_ib_vn_small(v, h->VM, gvn, h->s_lds_vn, st); })) != hipSuccess)
+          return e;
+        c.img = h->cn_img + (size_t)j * h->cn_nt * 256;
+        c.gate = gate;
+        c.unsat = early ? h->flags + (size_t)j * kShards : nullptr;
+        if ((e = h->timer.timed(0, st, [&] { return launch_ib_cn_small(c, h->CM, gcn, h->s_lds_cn, st); })) != hipSuccess)
+          return e;
+      }
+      return hipSuccess;
+    };
+    // replayed from a captured graph, unless per-launch timing is on (bench roofline) or graphs are off
+    if (h->s_graphs.on && !h->timer.on) HIPCHK(h->s_graphs.run(B, early ? 1 : 0, s, chain));
+    else HIPCHK(chain(s));
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     IbDecArgs dc{};
     dc.vin = h->vin; dc.ch8 = h->ch8; dc.img = h->dec_img; dc.iters = h->dL; dc.out = d_out; dc.out_dtype = out_dtype;
@@ -1156,6 +1220,8 @@ int ibl_float_create(const ibl_graph* g, int32_t kind, int32_t imax, double llr_
     const char* sb = getenv("IBL_SMALL_B");
     h->s_ok = priv == 0;
     h->small_b = h->s_ok ? (sb ? std::max(0, atoi(sb)) : kFlSmallBatchDefault) : 0;
+    const char* sg = getenv("IBL_SMALL_GRAPH");
+    h->s_graphs.on = !(sg && sg[0] == '0');
   }
   if ((rc = fold_alloc(h))) return bail(rc);
   *out = h;
@@ -1243,7 +1309,6 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     FlArgs send{};
     send.ch = h->chf; send.out = h->cin; send.start = g->vn_start; send.deg = g->vn_deg; send.tgt = g->tgt_vn;
     send.n_nodes = g->n_v; send.ldb = ldbs; send.B = B;
-    HIPCHK(launch_fl_send(send, h->prec, s));
     FlArgs cn{}, vn{};
     cn.in = h->cin; cn.start = g->cn_start; cn.deg = g->cn_deg; cn.tgt = g->tgt_cn; cn.ch = h->chf;
     vn.out = h->cin; vn.ch = h->chf; vn.start = g->vn_start; vn.deg = g->vn_deg; vn.tgt = g->tgt_vn;
@@ -1255,17 +1320,28 @@ int ibl_float_decode(ibl_float* h, const void* d_llr, int32_t llr_dtype, int32_t
     cn.ldb = vn.ldb = ldbs;
     cn.B = vn.B = B;
     const int gcn = grid_of(g->n_cn_task), gvn = grid_of(g->n_vn_task);
-    for (int j = 1; j < I; ++j) {
-      void* vb = (j & 1) ? h->vbuf1 : h->vbuf0;
-      cn.out = vb;
-      cn.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
-      cn.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-      HIPCHK(h->timer.timed(0, s, [&] { return launch_fl_cn_small(cn, h->kind, h->prec, g->dcm, gcn, s); }));
-      if (j == I - 1) break;   // the last variable pass feeds no output (as below)
-      vn.in = vb;
-      vn.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
-      HIPCHK(h->timer.timed(1, s, [&] { return launch_fl_vn_small(vn, h->prec, g->dvm, gvn, s); }));
-    }
+    // the pass chain (decoder buffers only): send, then {CN j, VN j} — replayed from a captured graph (ChainGraphs)
+    auto chain = [&](hipStream_t st) -> hipError_t {
+      hipError_t e = launch_fl_send(send, h->prec, st);
+      if (e != hipSuccess) return e;
+      FlArgs c = cn, v = vn;
+      for (int j = 1; j < I; ++j) {
+        void* vb = (j & 1) ? h->vbuf1 : h->vbuf0;
+        c.out = vb;
+        c.gate = (early && j >= 3) ? h->flags + (size_t)(j - 2) * kShards : nullptr;
+        c.unsat = early ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+        if ((e = h->timer.timed(0, st, [&] { return launch_fl_cn_small(c, h->kind, h->prec, g->dcm, gcn, st); })) != hipSuccess)
+          return e;
+        if (j == I - 1) break;   // the last variable pass feeds no output (as below)
+        v.in = vb;
+        v.gate = (early && j >= 2) ? h->flags + (size_t)(j - 1) * kShards : nullptr;
+        if ((e = h->timer.timed(1, st, [&] { return launch_fl_vn_small(v, h->prec, g->dvm, gvn, st); })) != hipSuccess)
+          return e;
+      }
+      return hipSuccess;
+    };
+    if (h->s_graphs.on && !h->timer.on) HIPCHK(h->s_graphs.run(B, early ? 1 : 0, s, chain));
+    else HIPCHK(chain(s));
     HIPCHK(launch_finalize(h->flags, I, early ? 1 : 0, h->dL, d_iters, s));
     FlDecArgs dc{};
     dc.vin0 = h->vbuf0; dc.vin1 = h->vbuf1; dc.ch = h->chf; dc.start = g->vn_start; dc.deg = g->vn_deg;
