@@ -56,17 +56,26 @@ def run(case, batches, B, gen_chunk=None):
     sec, sec_s = r.seconds[0], rs.seconds[0]
     # decode-only on the same decoder object, batch and early-stop setting: the drop-in decode of a channel
     # already resident in HBM, back to back (what bench.py's line measures), same number of batches
-    x = torch.empty((g.n_v, B), dtype=torch.uint8 if case.startswith("c4") else torch.float32, device="cuda")
+    # With early stop on, a batch's decode time depends on its frames: where the driver's batches fit in 1 GiB the
+    # decode-only line decodes as many fresh channels (consecutive Philox batches), else one resident channel again.
+    nb = r.blocks[0] // B
+    dt = torch.uint8 if case.startswith("c4") else torch.float32
     q = UniformQuantizer(sigma2_from_ebn0(ebn0, g.R_c), 16)
-    engine.channel_sample(x, q.cdf_t_given_x_equals_zero, 2, 0, llr=None if case.startswith("c4") else q.output_LLRs)
+    fresh = nb * g.n_v * B * (1 if case.startswith("c4") else 4) <= 1 << 30
+    xs = []
+    for k in range(nb if fresh else 1):
+        x = torch.empty((g.n_v, B), dtype=dt, device="cuda")
+        engine.channel_sample(x, q.cdf_t_given_x_equals_zero, 2, k * engine.philox_blocks(g.n_v, B),
+                              llr=None if case.startswith("c4") else q.output_LLRs)
+        xs.append(x)
     # (IB: u8 decisions, as the pipelined driver asks for them — the same cluster ids as the reference's int32)
     kw = {"out_dtype": torch.uint8} if case.startswith("c4") else {}
     fn = dec.decode_OpenCL if case.startswith("c4") else dec.decode_OpenCL_belief_propagation
-    fn(x, buffer_in=True, return_buffer=True, **kw)
+    fn(xs[0], buffer_in=True, return_buffer=True, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(r.blocks[0] // B):
-        fn(x, buffer_in=True, return_buffer=True, **kw)
+    for k in range(nb):
+        fn(xs[k % len(xs)], buffer_in=True, return_buffer=True, **kw)
     torch.cuda.synchronize()
     dec_only = r.blocks[0] / (time.perf_counter() - t0)
     value = r.blocks[0] / sec
@@ -76,8 +85,9 @@ def run(case, batches, B, gen_chunk=None):
             "sync_every": sync, "early_stop": True, "value": round(value, 1), "unit": "codewords/s",
             "seconds": round(sec, 4), "sync_driver": {"value": round(r.blocks[0] / sec_s, 1), "seconds": round(sec_s, 4),
                                                       "note": "cfg.pipeline=False: quantise -> decode -> count per batch"},
-            "decode_only": {"value": round(dec_only, 1),
-                            "note": "the same drop-in decode on a resident channel, back to back, same batches"},
+            "decode_only": {"value": round(dec_only, 1), "fresh_channels": fresh,
+                            "note": "the same drop-in decode on resident channels, back to back, same batch count "
+                                    "(fresh_channels: one per batch, else one channel decoded again)"},
             "vs_decode_only": round(value / dec_only, 4), "gen_chunk": BERConfig(**cfg).gen_chunk,
             "errors": r.errors[0], "errors_equal_sync_driver": True, "ber": float(r.BER_vector[0])}
 
